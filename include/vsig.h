@@ -1,0 +1,134 @@
+/* vsig — MI355X-native vector-signal DSP hot path, C ABI (libvsig.so).
+ *
+ * The reference (ramiyako/vector) is a pure-Python module whose DSP lives in
+ * utils.py and calls numpy/scipy directly; it has no FFI.  Each entry point
+ * below replaces one numpy/scipy call the reference makes on its hot path, and
+ * is what a ctypes / cffi binding in place of that call would bind
+ * (INTEGRATION.md shows the binding):
+ *
+ *   vsig_psd_*        scipy.signal.spectrogram(..., return_onesided=False,
+ *                     detrend=False, scaling='spectrum')      utils.py:281-291
+ *                     (+ fftshift of Sxx, utils.py:351, when shift = 1)
+ *   vsig_fir_*        np.convolve(x, taps, 'full')[:len(x)] then x[::decim]
+ *                     (reference idioms utils.py:802,816 and utils.py:194)
+ *   vsig_correlate_*  np.correlate(signal2, signal1, mode) in
+ *                     cross_correlate_signals                  utils.py:1284-1285
+ *   vsig_xcorr_*      the same, streaming form with a fixed template, fused
+ *                     with find_correlation_peak               utils.py:1321-1334
+ *   vsig_peak_*       find_correlation_peak's |c| argmax / mean / std
+ *                                                               utils.py:1321-1334
+ *
+ * Conventions
+ *   - complex data is interleaved float32 pairs (numpy complex64 layout);
+ *     complex128 only where stated.
+ *   - "_dev" functions take device pointers and enqueue on the context's
+ *     stream (vsig_set_stream); they do not synchronise.  Host-pointer
+ *     functions copy in, compute and copy out synchronously.
+ *   - the caller allocates every output; the library never frees caller
+ *     memory.  Output sizes follow the formulas in the comments.
+ *   - every function returns VSIG_OK (0) or a negative status; nothing throws
+ *     across the ABI.  vsig_last_error(ctx) gives a message.
+ *   - one context per host thread.
+ */
+#ifndef VSIG_H
+#define VSIG_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define VSIG_OK 0
+#define VSIG_E_INVALID -1     /* bad argument (size, mode, null pointer ...) */
+#define VSIG_E_HIP -2         /* HIP runtime error */
+#define VSIG_E_NOMEM -3       /* device allocation failed */
+#define VSIG_E_UNSUPPORTED -4 /* size outside what the kernels implement */
+#define VSIG_E_NODEVICE -5    /* no HIP device */
+
+#define VSIG_MODE_VALID 0
+#define VSIG_MODE_FULL 1
+#define VSIG_MODE_SAME 2
+
+#define VSIG_DTYPE_C128 0
+#define VSIG_DTYPE_C64 1
+#define VSIG_DTYPE_F64 2
+#define VSIG_DTYPE_F32 3
+
+typedef struct vsig_ctx vsig_ctx;
+typedef struct vsig_fir vsig_fir;
+typedef struct vsig_xcorr vsig_xcorr;
+
+/* Result of a |c| peak reduction (find_correlation_peak, utils.py:1321-1334).
+ * index: first maximum of |c|; peak: |c[index]|; sums over every element. */
+typedef struct vsig_peak_t {
+  double peak;
+  int64_t index;
+  double sum_abs;
+  double sum_abs2;
+} vsig_peak_t;
+
+int vsig_version(void);
+const char* vsig_errstr(int status);
+
+/* ---- context ------------------------------------------------------------- */
+int vsig_init(int device, vsig_ctx** out);
+void vsig_free(vsig_ctx* ctx);
+const char* vsig_last_error(const vsig_ctx* ctx);
+/* hip_stream: a hipStream_t, or NULL for the context's own stream. */
+int vsig_set_stream(vsig_ctx* ctx, void* hip_stream);
+int vsig_synchronize(vsig_ctx* ctx);
+/* Per-kernel timing with HIP events on the context stream (for bench.py):
+ * enable, run, then read the mean duration in ms of each kernel family. */
+int vsig_timing_enable(vsig_ctx* ctx, int on);
+int vsig_timing_read(vsig_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches);
+int vsig_timing_reset(vsig_ctx* ctx);
+
+/* ---- spectrum: Sxx[f, k] = |sum_{i<nperseg} w[i] x[f*hop + i] e^{-2 pi j k i / nfft}|^2 * scale
+ * nfft: power of two in [64, 16384]; nframes = (n - nperseg) / hop + 1;
+ * sxx is frame-major float32 [nframes][nfft] (Sxx of scipy is its transpose);
+ * shift = 1 stores bin k at (k + nfft/2) % nfft (np.fft.fftshift).
+ * _dev only: stride reads sample i at x[i*stride] (n counts strided samples),
+ * which folds create_spectrogram's sig[::factor] (utils.py:194) into the load. */
+int vsig_psd_c64_dev(vsig_ctx* ctx, const void* x, int64_t n, int64_t stride, const float* win,
+                     int32_t nperseg, int64_t hop, int32_t nfft, float scale, int32_t shift,
+                     float* sxx, int64_t nframes);
+int vsig_psd_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* win, int32_t nperseg,
+                 int64_t hop, int32_t nfft, float scale, int32_t shift, float* sxx,
+                 int64_t nframes);
+
+/* ---- FIR: y[g] = sum_{m<ntaps} h[m] x[g*decim - m] (x = 0 outside [0, n)),
+ * g in [0, ceil(n/decim)).  Taps complex64 on the host (real taps: imag = 0);
+ * ntaps in [1, 8192]. */
+int vsig_fir_create(vsig_ctx* ctx, const void* taps, int32_t ntaps, int32_t decim, vsig_fir** out);
+void vsig_fir_free(vsig_fir* fir);
+int vsig_fir_exec_dev(vsig_fir* fir, const void* x, int64_t n, void* y, int64_t ny);
+int vsig_fir_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* taps, int32_t ntaps,
+                 int32_t decim, void* y, int64_t ny);
+
+/* ---- streaming correlation with a fixed template p of length L (<= 8192):
+ * c[o] = sum_{k<L} s[o - off + k] conj(p[k]), mode VALID (off = 0, nout = n-L+1)
+ * or FULL (off = L-1, nout = n+L-1).  c may be NULL (peak only).  peak_dev: a
+ * device vsig_peak (may be NULL); peak = max |c|, sums over all nout outputs. */
+int vsig_xcorr_create(vsig_ctx* ctx, const void* tmpl, int32_t L, vsig_xcorr** out);
+void vsig_xcorr_free(vsig_xcorr* xc);
+int vsig_xcorr_exec_dev(vsig_xcorr* xc, const void* s, int64_t n, int32_t mode, void* c,
+                        vsig_peak_t* peak_dev);
+
+/* ---- general correlation, np.correlate(a, v, mode) semantics for any length
+ * order (min(na, nv) <= 8192): output length full na+nv-1, valid
+ * |na-nv|+1, same max(na, nv).  All pointers device (dev) or host. */
+int vsig_correlate_c64_dev(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,
+                           int32_t mode, void* c, vsig_peak_t* peak_dev);
+int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,
+                       int32_t mode, void* c, vsig_peak_t* peak);
+
+/* ---- |c| reduction in double precision over an array of dtype VSIG_DTYPE_*:
+ * index of the first max of |c|, the max, sum |c|, sum |c|^2. */
+int vsig_peak_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev);
+int vsig_peak(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VSIG_H */

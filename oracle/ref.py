@@ -1,0 +1,327 @@
+"""CPU oracle for the vector-signal DSP hot path — TEST INFRASTRUCTURE ONLY.
+
+This module is the parity checker, never the product.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it.  The product (``vector_amd``) must never import or call anything here; it
+fails loudly when its HIP library is missing instead of falling back to a CPU
+path.
+
+It restates, in plain NumPy/SciPy, the semantics of the reference's DSP
+functions (ramiyako/vector ``utils.py``, snapshot 2025-07-18).  The reference's
+arithmetic itself lives in third-party code that is *not* vendored under
+``/root/reference``: numpy 2.2.6 (``np.correlate`` -> ``multiarray.correlate2``,
+``np.convolve`` -> ``multiarray.correlate``, ``numpy/_core/numeric.py:693-869``)
+and scipy 1.15.3 (``scipy.signal.spectrogram`` -> ``_spectral_helper`` ->
+``_fft_helper`` -> pocketfft, ``scipy/signal/_spectral_py.py:816-2205``).
+Requirements pin only lower bounds (``requirements.txt``: numpy>=1.21,
+scipy>=1.7).  This oracle calls those same library routines, so its numerics are
+the reference's numerics.
+
+Pinning: every function below is checked against golden vectors produced by
+importing the reference's own ``utils`` in the build container
+(``tests/golden/make_golden.py`` -> ``tests/golden/*.npz``) and against the
+known answers of the reference's tests (``tests/test_utils.py:24-34``,
+``test_packet_transplant.py:40-68``).  ``fir_filter`` and ``pfb_channelize`` have
+no reference function: they are pinned by numpy semantics
+only ("parity unpinned" at the reference level).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.signal
+
+__all__ = [
+    "spectrum", "spectrogram_params", "create_spectrogram", "normalize_spectrogram",
+    "cross_correlate_signals", "find_correlation_peak", "xcorr_peak",
+    "find_packet_location_in_vector", "find_packet_start", "detect_packet_bounds",
+    "fir_filter", "stride_decimate", "pfb_channelize", "synth_iq", "qpsk_preamble",
+]
+
+
+# ---------------------------------------------------------------------------
+# spectrum — utils.py:281-291 (scipy.signal.spectrogram, two-sided, 'spectrum')
+# ---------------------------------------------------------------------------
+def spectrum(x, fs=1.0, window="hann", nperseg=256, noverlap=None, nfft=None):
+    """``scipy.signal.spectrogram`` exactly as the reference calls it
+    (utils.py:281-291): ``return_onesided=False, detrend=False,
+    scaling='spectrum'``.  Returns ``(f, t, Sxx)``; ``Sxx`` is (nfft, nframes)."""
+    return scipy.signal.spectrogram(
+        x, fs=fs, window=window, nperseg=nperseg, noverlap=noverlap, nfft=nfft,
+        return_onesided=False, detrend=False, scaling="spectrum")
+
+
+def spectrogram_params(n, sr, max_samples=2_000_000, time_resolution_us=1,
+                       adaptive_resolution=True):
+    """Host-side parameter selection of ``create_spectrogram``
+    (utils.py:183-276), restated without the STFT call.
+
+    Returns a dict with factor, fs, nsig (samples after stride decimation),
+    window, nperseg, noverlap, nfft, heavy.
+    """
+    if n == 0:
+        raise ValueError("Signal is empty")
+    heavy = n > 5_000_000                                     # utils.py:184
+    if heavy:
+        max_samples = min(max_samples, 1_000_000)             # utils.py:188
+        time_resolution_us = max(time_resolution_us, 20)      # utils.py:189
+    if n > max_samples:                                       # utils.py:192-195
+        factor = int(np.ceil(n / max_samples))
+        nsig = len(range(0, n, factor))
+        fs = sr / factor
+    else:
+        factor = 1
+        nsig = n
+        fs = sr
+    dur_us = nsig / fs * 1e6                                  # utils.py:203
+    if adaptive_resolution:                                   # utils.py:206-234
+        if dur_us <= 50:
+            base_window = max(32, min(nsig // 12, 128))
+            time_resolution_us = min(time_resolution_us, dur_us / 10)
+            frf = 1.2
+        elif dur_us <= 500:
+            base_window = max(64, min(nsig // 10, 256))
+            time_resolution_us = min(time_resolution_us, dur_us / 20)
+            frf = 1.2
+        elif dur_us <= 5000:
+            base_window = max(128, min(nsig // 8, 512))
+            time_resolution_us = min(time_resolution_us, 10)
+            frf = 1.5
+        else:
+            base_window = max(256, min(nsig // 6, 1024))
+            time_resolution_us = min(time_resolution_us, 20)
+            frf = 1.5
+            if heavy:
+                base_window = min(base_window, 512)
+                time_resolution_us = max(time_resolution_us, 50)
+                frf = 1.2
+    else:
+        base_window = max(128, min(nsig // 8, 512))
+        frf = 1.2
+    if time_resolution_us is not None:                        # utils.py:237-252
+        step = max(1, int(round(fs * time_resolution_us / 1e6)))
+        step = min(step, nsig // 10)
+        step = max(1, step)
+        window_size = max(base_window, step * 2)
+        window_size = min(window_size, nsig)
+        if heavy:
+            overlap = max(0, window_size - step * 2)
+        else:
+            overlap = max(0, window_size - step)
+    else:                                                     # utils.py:253-259
+        window_size = min(base_window, nsig)
+        overlap = int(window_size * 0.75) if heavy else int(window_size * 0.90)
+    nfft = max(256, int(2 ** np.ceil(np.log2(window_size * frf))))  # :262
+    nfft = min(nfft, 1024) if heavy else max(nfft, 512)       # utils.py:265-268
+    window = "hann" if heavy else "blackmanharris"            # utils.py:273-276
+    return dict(factor=factor, fs=fs, nsig=nsig, window=window,
+                nperseg=window_size, noverlap=overlap, nfft=nfft, heavy=heavy)
+
+
+def create_spectrogram(sig, sr, center_freq=0, max_samples=2_000_000,
+                       time_resolution_us=1, adaptive_resolution=True):
+    """Restatement of ``create_spectrogram`` (utils.py:161-353): parameter
+    logic, stride decimation, STFT, the two fallback branches and fftshift."""
+    sig = np.asarray(sig)
+    p = spectrogram_params(len(sig), sr, max_samples, time_resolution_us,
+                           adaptive_resolution)
+    factor, fs = p["factor"], p["fs"]
+    if factor > 1:
+        sig = sig[::factor]
+    try:                                                      # utils.py:279-313
+        freqs, times, Sxx = spectrum(sig, fs, p["window"], p["nperseg"],
+                                     p["noverlap"], p["nfft"])
+    except Exception:
+        ws = min(256, len(sig))
+        freqs, times, Sxx = spectrum(sig, fs, "hann", ws, ws // 2, 512)
+    if np.max(Sxx) == 0:                                      # utils.py:316-347
+        ws = min(64, len(sig) // 4)
+        try:
+            freqs, times, Sxx = spectrum(sig, fs, "hann", ws, ws // 4, max(128, ws))
+        except Exception:
+            freqs, times, Sxx = spectrum(sig, fs, "boxcar", 32, 16, 64)
+    freqs = np.fft.fftshift(freqs) * factor + center_freq    # utils.py:350
+    Sxx = np.fft.fftshift(Sxx, axes=0)                        # utils.py:351
+    return freqs, times, Sxx
+
+
+def normalize_spectrogram(Sxx, low_percentile=10.0, high_percentile=95.0,
+                          max_dynamic_range=25):
+    """Restatement of ``normalize_spectrogram`` (utils.py:356-404), minus prints."""
+    if Sxx.size == 0:
+        return np.array([]), 0, 0
+    a = np.abs(Sxx)
+    nf = np.percentile(a[a > 0], 5) if np.any(a > 0) else 1e-12
+    nf = max(nf, 1e-12)
+    db = 10 * np.log10(a + nf)
+    try:
+        vmin = np.percentile(db, low_percentile)
+        vmax = np.percentile(db, high_percentile)
+    except Exception:
+        vmin, vmax = np.min(db), np.max(db)
+    if np.isnan(vmin) or np.isnan(vmax) or vmax <= vmin:
+        vmin, vmax = np.min(db), np.max(db)
+        if vmax <= vmin:
+            vmax = vmin + max_dynamic_range
+    rng = vmax - vmin
+    if rng > max_dynamic_range:
+        vmin = vmax - max_dynamic_range
+    elif rng < 20:
+        mid = (vmax + vmin) / 2
+        vmin, vmax = mid - 10, mid + 10
+    vmin = max(vmin, -120)
+    return db, vmin, vmax
+
+
+# ---------------------------------------------------------------------------
+# correlation — utils.py:1258-1342, 1372-1434, 793-795
+# ---------------------------------------------------------------------------
+def cross_correlate_signals(signal1, signal2, mode="full"):
+    """utils.py:1258-1295: upcast to complex128, ``np.correlate(signal2,
+    signal1, mode)`` (conjugates signal1), plus the lag axis (incl. the
+    'same'-mode lag-length quirk)."""
+    s1 = np.asarray(signal1).astype(np.complex128)
+    s2 = np.asarray(signal2).astype(np.complex128)
+    c = np.correlate(s2, s1, mode=mode)
+    if mode == "full":
+        lags = np.arange(-len(s1) + 1, len(s2))
+    elif mode == "same":
+        lags = np.arange(-len(s1) // 2, len(s1) // 2 + len(s1) % 2)
+    else:
+        lags = np.arange(len(s2) - len(s1) + 1)
+    return c, lags
+
+
+def find_correlation_peak(correlation, lags, threshold_ratio=0.5):
+    """utils.py:1298-1342: first-max argmax of |c|, z-score confidence / 10
+    clipped to [0, 1] (population std)."""
+    a = np.abs(correlation)
+    i = int(np.argmax(a))
+    peak = a[i]
+    m, s = np.mean(a), np.std(a)
+    conf = float(np.clip((peak - m) / s / 10.0, 0.0, 1.0)) if s > 0 else 0.0
+    if peak < threshold_ratio * np.max(a):
+        conf = 0.0
+    return lags[i], peak, conf
+
+
+def xcorr_peak(stream, preamble, mode="valid"):
+    """Fused form used by the sync stage: correlate + find_correlation_peak.
+    Returns (argmax index into the correlation, peak_lag, peak |c|, sum|c|,
+    sum|c|^2, confidence) computed in complex128 like the reference."""
+    c, lags = cross_correlate_signals(preamble, stream, mode)
+    a = np.abs(c)
+    i = int(np.argmax(a))
+    lag, peak, conf = find_correlation_peak(c, lags)
+    return i, int(lag), float(peak), float(a.sum()), float((a * a).sum()), conf
+
+
+def find_packet_location_in_vector(vector, packet_signal, reference_segment,
+                                   search_window=None, correlation_threshold=0.5):
+    """utils.py:1372-1434."""
+    if search_window is None:
+        s0, s1 = 0, len(vector)
+    else:
+        s0, s1 = search_window
+        s0, s1 = max(0, s0), min(len(vector), s1)
+    vc, vl = cross_correlate_signals(reference_segment, vector[s0:s1])
+    vlag, _, vconf = find_correlation_peak(vc, vl, correlation_threshold)
+    pc, pl = cross_correlate_signals(reference_segment, packet_signal)
+    plag, _, pconf = find_correlation_peak(pc, pl, correlation_threshold)
+    return s0 + vlag - plag, 0, min(vconf, pconf)
+
+
+def find_packet_start(signal, template=None, threshold_ratio=0.2, window_size=None):
+    """utils.py:784-809 (template branch: argmax of |x| (*) |t| 'valid';
+    energy branch: boxcar-smoothed |x|^2, median-of-first-10% threshold)."""
+    if template is not None:
+        c = np.correlate(np.abs(signal), np.abs(template), mode="valid")
+        return int(np.argmax(c))
+    e = np.abs(signal) ** 2
+    if window_size is None:
+        window_size = max(1, int(0.02 * len(signal)))
+    w = np.ones(max(1, window_size)) / max(1, window_size)
+    sm = np.convolve(e, w, mode="same")
+    noise = np.median(sm[: len(sm) // 10])
+    thr = noise + threshold_ratio * (np.max(sm) - noise)
+    idx = np.where(sm >= thr)[0]
+    return int(idx[0]) if len(idx) > 0 else 0
+
+
+def detect_packet_bounds(signal, sample_rate, threshold_ratio=0.2):
+    """utils.py:811-825."""
+    e = np.abs(signal) ** 2
+    w = max(1, int(sample_rate // 1_000_000))
+    sm = np.convolve(e, np.ones(w) / w, mode="same")
+    noise = np.median(sm[: max(1, len(sm) // 10)])
+    thr = noise + threshold_ratio * (sm.max() - noise)
+    idx = np.where(sm >= thr)[0]
+    if len(idx) == 0:
+        return 0, len(signal)
+    return idx[0], idx[-1]
+
+
+# ---------------------------------------------------------------------------
+# filter / decimate — reference idioms np.convolve (utils.py:802,816) and
+# x[::factor] (utils.py:194).  No reference FIR exists: parity unpinned at the
+# reference level, pinned by numpy semantics.
+# ---------------------------------------------------------------------------
+def fir_filter(x, taps, decim=1):
+    """Causal FIR ``np.convolve(x, taps, 'full')[:len(x)]`` then ``[::decim]``."""
+    x = np.asarray(x)
+    y = np.convolve(x, np.asarray(taps), mode="full")[: len(x)]
+    return y[::decim] if decim > 1 else y
+
+
+def stride_decimate(x, factor):
+    """utils.py:192-195 / heavy_packet_optimizer.py:164-168."""
+    return np.asarray(x)[::factor]
+
+
+def pfb_channelize(x, proto, nchan):
+    """Critically sampled polyphase filter-bank analysis channelizer
+    (BASELINE config 4; no reference counterpart — parity unpinned).
+    Nearest reference analogue: the FFT brick-wall channel split
+    ``vector_analyzer/split_channels.py:15-44``.
+
+    Windowed pre-sum PFB (C channels, P = len(proto) // C taps per branch):
+        z_m[p]  = sum_{q=0}^{P-1} h[q*C + p] * x[m*C + q*C + p]
+        y[k, m] = sum_{p=0}^{C-1} z_m[p] * exp(-2j*pi*k*p/C)
+    for m = 0 .. (len(x) - P*C) // C.  Output (C, M) complex64, computed here
+    in complex128.
+    """
+    x = np.asarray(x, dtype=np.complex128)
+    h = np.asarray(proto, dtype=np.float64)
+    C = int(nchan)
+    P = len(h) // C
+    if P * C != len(h):
+        raise ValueError("len(proto) must be a multiple of nchan")
+    M = (len(x) - P * C) // C + 1
+    if M <= 0:
+        return np.zeros((C, 0), np.complex64)
+    frames = np.lib.stride_tricks.sliding_window_view(x, P * C)[::C][:M]
+    z = (frames * h[None, :]).reshape(M, P, C).sum(axis=1)     # (M, C)
+    return np.fft.fft(z, axis=1).T.astype(np.complex64)
+
+
+# ---------------------------------------------------------------------------
+# synthetic inputs — SURVEY.md §8(d)
+# ---------------------------------------------------------------------------
+TONES = ((1.0, 0.05), (0.5, 0.11), (0.25, -0.20))
+
+
+def synth_iq(n, seed=20250718, chunk=None, offset=0):
+    """x[n] = sum_i A_i e^{j 2 pi f_i n} + w[n], w ~ CN(0, 1), complex64."""
+    rng = np.random.default_rng(seed if chunk is None else [seed, chunk])
+    idx = np.arange(offset, offset + n, dtype=np.float64)
+    x = np.zeros(n, np.complex128)
+    for a, f in TONES:
+        x += a * np.exp(2j * np.pi * f * idx)
+    w = (rng.standard_normal(n) + 1j * rng.standard_normal(n)) * np.sqrt(0.5)
+    return (x + w).astype(np.complex64)
+
+
+def qpsk_preamble(L=4096, seed=4096):
+    """L QPSK symbols (+-1 +-j)/sqrt(2), complex64."""
+    rng = np.random.default_rng(seed)
+    b = rng.integers(0, 2, size=(2, L))
+    return (((2 * b[0] - 1) + 1j * (2 * b[1] - 1)) / np.sqrt(2)).astype(np.complex64)

@@ -1,0 +1,244 @@
+"""Generate the golden fixtures in tests/golden/ from the REFERENCE itself.
+
+Run in the build container only (needs /root/reference, read-only):
+
+    PYTHONDONTWRITEBYTECODE=1 MPLBACKEND=Agg python tests/golden/make_golden.py
+
+It imports the reference's ``utils`` module (ramiyako/vector ``utils.py``) and
+records inputs + outputs of the hot-path functions as small ``.npz`` files.
+Nothing from the reference's source is copied; only data (inputs, outputs,
+parameters) is stored.  The GPU box never runs this script.
+
+Fixture inventory (SURVEY.md §8(c) golden set G1-G5):
+  spec_params.npz      create_spectrogram parameter logic (utils.py:161-276)
+                       recorded from the reference's own scipy call, N up to 2**28
+  spec_<case>.npz      create_spectrogram(sig, sr) outputs (f, t, Sxx) for small inputs
+                       incl. the reference's real data files (data/*.mat, sample_vector.mat)
+  stft_<case>.npz      the scipy.signal.spectrogram call the reference makes
+                       (utils.py:281-291) at BASELINE C1/C2 shapes (reduced N)
+  xcorr_small.npz      cross_correlate_signals full/valid/same arrays (utils.py:1258-1295)
+                       + find_correlation_peak (utils.py:1298-1342)
+  xcorr_peak.npz       L=4096 QPSK preamble in a 2**17 stream: peak lag/value/confidence
+  packet.npz           find_packet_start / detect_packet_bounds /
+                       find_packet_location_in_vector results (utils.py:784-825, 1372-1434)
+  fir.npz              np.convolve(x, taps)[:N][::D] (no reference FIR: numpy-pinned)
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import scipy
+import scipy.io as sio
+import scipy.signal
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF = "/root/reference"
+sys.path.insert(0, os.path.join(HERE, "..", ".."))
+sys.path.insert(0, REF)
+
+import utils as refutils  # noqa: E402  (the reference)
+
+from oracle.ref import qpsk_preamble, synth_iq  # noqa: E402  (seeded generators only)
+
+META = dict(numpy=np.__version__, scipy=scipy.__version__,
+            reference="ramiyako/vector@2025-07-18 utils.py")
+
+
+def save(name, **arrs):
+    arrs.update({f"meta_{k}": np.array(v) for k, v in META.items()})
+    np.savez_compressed(os.path.join(HERE, name), **arrs)
+    print("wrote", name, {k: getattr(v, "shape", None) for k, v in arrs.items()
+                          if not k.startswith("meta_")})
+
+
+class Recorder:
+    """Wraps scipy.signal.spectrogram inside the reference module to record the
+    exact arguments create_spectrogram passes (optionally skipping the call)."""
+
+    def __init__(self, dry=False):
+        self.calls = []
+        self.dry = dry
+        self.real = scipy.signal.spectrogram
+
+    def __call__(self, x, fs=1.0, window="hann", nperseg=None, noverlap=None,
+                 nfft=None, **kw):
+        self.calls.append(dict(n=len(x), fs=fs, window=window, nperseg=nperseg,
+                               noverlap=noverlap, nfft=nfft, kw=kw))
+        if self.dry:
+            nfr = max(1, (len(x) - nperseg) // (nperseg - noverlap) + 1)
+            return (np.fft.fftfreq(nfft, 1 / fs), np.arange(nfr, dtype=float),
+                    np.ones((nfft, nfr), np.float32))
+        return self.real(x, fs=fs, window=window, nperseg=nperseg,
+                         noverlap=noverlap, nfft=nfft, **kw)
+
+
+def record_spectrogram(sig, sr, dry=False, **kw):
+    rec = Recorder(dry)
+    orig = refutils.scipy.signal.spectrogram
+    refutils.scipy.signal.spectrogram = rec
+    try:
+        out = refutils.create_spectrogram(sig, sr, **kw)
+    finally:
+        refutils.scipy.signal.spectrogram = orig
+    return out, rec.calls
+
+
+def gen_spec_params():
+    cases = []
+    for n in (500, 2_000, 10_000, 50_000, 140_000, 2 ** 16, 2 ** 20, 1_500_000,
+              3_000_000, 10_000_000, 15_000_000, 2 ** 28):
+        for sr in (56e6, 10e6, 8000.0):
+            cases.append((n, sr, 2_000_000, 1, True))
+    cases += [(10_000_000, 56e6, 1_000_000, 50, True), (2 ** 20, 56e6, 2_000_000, 1, False),
+              (3_000_000, 56e6, 5_000_000, 10, True), (500_000, 56e6, 2_000_000, 25, True)]
+    rows = []
+    for n, sr, ms, tr, ad in cases:
+        sig = np.broadcast_to(np.complex64(1 + 1j), (n,))
+        (_, _, _), calls = record_spectrogram(sig, sr, dry=True, max_samples=ms,
+                                              time_resolution_us=tr,
+                                              adaptive_resolution=ad)
+        c = calls[0]
+        rows.append((n, sr, ms, tr, int(ad), c["n"], c["fs"], c["nperseg"],
+                     c["noverlap"], c["nfft"], 1 if c["window"] == "hann" else 0))
+    a = np.array(rows, dtype=np.float64)
+    save("spec_params.npz", table=a,
+         columns=np.array("n sr max_samples time_res_us adaptive nsig fs nperseg "
+                          "noverlap nfft window_is_hann".split()))
+
+
+def frame_subset(nframes, keep=96):
+    """Frames stored in full (first, last, and evenly spaced); every frame's
+    float64 sum is stored too, so the whole output is still checked."""
+    if nframes <= keep:
+        return np.arange(nframes)
+    return np.unique(np.concatenate([np.arange(8), np.arange(nframes - 8, nframes),
+                                     np.linspace(0, nframes - 1, keep - 16).astype(int)]))
+
+
+def gen_spec_outputs():
+    cases = {}
+    cases["synth16k_56M"] = (synth_iq(16384, seed=1), 56e6)
+    cases["synth64k_56M"] = (synth_iq(2 ** 16, seed=2), 56e6)
+    cases["tone_8k"] = (refutils.apply_frequency_shift(
+        refutils.generate_sample_packet(0.1, 8000, 1000), 500, 8000), 8000.0)
+    sv = sio.loadmat(os.path.join(REF, "sample_vector.mat"), squeeze_me=True)["Y"]
+    cases["sample_vector_56M"] = (np.asarray(sv).ravel().astype(np.complex64), 56e6)
+    pk = sio.loadmat(os.path.join(REF, "data", "packet_3_bpsk.mat"), squeeze_me=True)["Y"]
+    cases["packet3_bpsk_56M"] = (np.asarray(pk).ravel().astype(np.complex64), 56e6)
+    cases["sparse_zeros"] = (np.zeros(4096, np.complex64), 56e6)
+    for name, (sig, sr) in cases.items():
+        (f, t, S), calls = record_spectrogram(sig, sr)
+        c = calls[-1]
+        S = S.astype(np.float32)
+        sel = frame_subset(S.shape[1])
+        save(f"spec_{name}.npz", x=sig, sr=np.float64(sr), f=f, t=t,
+             Sxx_sel=S[:, sel], sel=sel, frame_sum=S.astype(np.float64).sum(axis=0),
+             shape=np.array(S.shape), nperseg=c["nperseg"], noverlap=c["noverlap"],
+             nfft=c["nfft"], window=np.array(c["window"]), ncalls=len(calls))
+
+
+def gen_stft():
+    # BASELINE C1 shape (reduced N) and C2 shape (reduced N), exactly the kwargs
+    # the reference passes at utils.py:281-291.
+    for name, n, win, nps, nov, nfft in (("c1_1024", 2 ** 16, "hann", 1024, 0, 1024),
+                                         ("c2_8192", 2 ** 17, "hann", 8192, 0, 8192),
+                                         ("bh_ovl", 2 ** 15, "blackmanharris", 1000, 900, 2048),
+                                         ("box_small", 3000, "boxcar", 32, 16, 64)):
+        x = synth_iq(n, seed=n + nps)
+        f, t, S = scipy.signal.spectrogram(x, fs=56e6, window=win, nperseg=nps,
+                                           noverlap=nov, nfft=nfft,
+                                           return_onesided=False, detrend=False,
+                                           scaling="spectrum")
+        save(f"stft_{name}.npz", x=x, f=f, t=t, Sxx=S.astype(np.float32),
+             nperseg=nps, noverlap=nov, nfft=nfft, window=np.array(win))
+
+
+def gen_xcorr():
+    rng = np.random.default_rng(7)
+    s1 = (rng.standard_normal(64) + 1j * rng.standard_normal(64)).astype(np.complex64)
+    s2 = (rng.standard_normal(2048) + 1j * rng.standard_normal(2048)).astype(np.complex64)
+    s2[700:764] += 3 * s1
+    out = dict(s1=s1, s2=s2)
+    for mode in ("full", "valid", "same"):
+        c, lags = refutils.cross_correlate_signals(s1, s2, mode=mode)
+        out[f"c_{mode}"] = c
+        out[f"lags_{mode}"] = lags
+        try:
+            lag, val, conf = refutils.find_correlation_peak(c, lags)
+            out[f"peak_{mode}"] = np.array([lag, val, conf], np.float64)
+        except IndexError:
+            # 'same' mode: len(lags) = L + L%2 != len(c) (utils.py:1290-1291), so
+            # the reference's find_correlation_peak raises IndexError whenever the
+            # argmax lies beyond len(lags).  Recorded as behaviour to reproduce.
+            out[f"peak_{mode}_raises"] = np.array("IndexError")
+    # zero-lag identity case (test_packet_transplant.py:57-68)
+    c, lags = refutils.cross_correlate_signals(s1, s1)
+    out["self_peak"] = np.array(refutils.find_correlation_peak(c, lags), np.float64)
+    save("xcorr_small.npz", **out)
+
+    L, n, k0 = 4096, 2 ** 17, 100_003
+    pre = qpsk_preamble(L)
+    x = synth_iq(n, seed=11)
+    x[k0:k0 + L] += pre
+    c, lags = refutils.cross_correlate_signals(pre, x, mode="valid")
+    a = np.abs(c)
+    lag, val, conf = refutils.find_correlation_peak(c, lags)
+    save("xcorr_peak.npz", x=x, pre=pre, k0=k0, peak_lag=lag, peak_val=val,
+         conf=conf, sum_abs=a.sum(), sum_abs2=(a * a).sum(),
+         top2=np.sort(a)[-2:])
+    c, lags = refutils.cross_correlate_signals(pre, x, mode="full")
+    lag, val, conf = refutils.find_correlation_peak(c, lags)
+    save("xcorr_peak_full.npz", peak_lag=lag, peak_val=val, conf=conf)
+
+
+def gen_packet():
+    out = {}
+    # reference tests' known answers (tests/test_utils.py:24-34)
+    sig = np.concatenate([np.zeros(100), np.ones(50), np.zeros(20)])
+    out["energy_start"] = refutils.find_packet_start(sig)
+    tmpl = np.array([1.0, 1.0, 1.0])
+    sig2 = np.concatenate([np.zeros(10), tmpl, np.zeros(5)])
+    out["template_start"] = refutils.find_packet_start(sig2, template=tmpl)
+    # synthetic burst
+    rng = np.random.default_rng(3)
+    n = 200_000
+    x = (0.01 * (rng.standard_normal(n) + 1j * rng.standard_normal(n))).astype(np.complex64)
+    x[61_234:141_000] += np.exp(2j * np.pi * 0.013 * np.arange(141_000 - 61_234))
+    out["burst_x"] = x
+    out["burst_start"] = refutils.find_packet_start(x)
+    out["burst_bounds"] = np.array(refutils.detect_packet_bounds(x, 56e6))
+    tm = x[61_234:61_234 + 512].copy()
+    out["burst_template_start"] = refutils.find_packet_start(x[:80_000], template=tm)
+    # transplant localisation with a unique-peak QPSK reference
+    ref = qpsk_preamble(256, seed=99)
+    packet = (0.05 * (rng.standard_normal(4000) + 1j * rng.standard_normal(4000))).astype(np.complex64)
+    packet[500:756] += ref
+    vec = (0.05 * (rng.standard_normal(30000) + 1j * rng.standard_normal(30000))).astype(np.complex64)
+    vec[12_345:12_601] += ref
+    out["loc_ref"], out["loc_packet"], out["loc_vector"] = ref, packet, vec
+    out["loc_result"] = np.array(refutils.find_packet_location_in_vector(vec, packet, ref), np.float64)
+    out["loc_result_win"] = np.array(refutils.find_packet_location_in_vector(
+        vec, packet, ref, search_window=(10_000, 20_000)), np.float64)
+    save("packet.npz", **out)
+
+
+def gen_fir():
+    x = synth_iq(2 ** 16, seed=5)
+    t63 = scipy.signal.firwin(63, 0.25).astype(np.float32)
+    t255 = scipy.signal.firwin(255, 0.2).astype(np.float32)
+    out = dict(x=x, taps63=t63, taps255=t255)
+    for nt, t in ((63, t63), (255, t255)):
+        for d in (1, 4):
+            out[f"y{nt}_d{d}"] = np.convolve(x, t, mode="full")[: len(x)][::d]
+    save("fir.npz", **out)
+
+
+if __name__ == "__main__":
+    gen_spec_params()
+    gen_spec_outputs()
+    gen_stft()
+    gen_xcorr()
+    gen_packet()
+    gen_fir()

@@ -1,0 +1,14 @@
+"""vector_amd — MI355X-native DSP hot path of ramiyako/vector.
+
+FIR -> decimate -> block FFT / PSD -> sliding cross-correlation, as hand-written
+CDNA4 HIP kernels in libvsig.so (C ABI, include/vsig.h), behind the reference's
+own Python call signatures (utils.py).  No CPU fallback: without the library or
+a HIP device every call raises ``VsigUnavailable``.
+"""
+from ._lib import VsigError, VsigUnavailable, get_context, load_library  # noqa: F401
+from .dsp import (Correlator, FirFilter, correlate, correlate_peak,  # noqa: F401
+                  cross_correlate_signals, filter, find_correlation_peak,
+                  find_packet_location_in_vector, fir_filter, peak_stats, spectrum)
+from .spectrogram import create_spectrogram, spectrogram_params  # noqa: F401
+
+__version__ = "0.1.0"

@@ -1,0 +1,142 @@
+"""ctypes binding of libvsig.so (include/vsig.h) and per-device contexts.
+
+The product path has no CPU fallback: if the library is missing or no HIP
+device is present, every compute call raises ``VsigUnavailable``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch  # loaded first: libvsig.so then binds torch's HIP runtime (same soname)
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libvsig.so")
+
+VSIG_OK = 0
+MODES = {"valid": 0, "full": 1, "same": 2}
+DTYPES = {"c128": 0, "c64": 1, "f64": 2, "f32": 3}
+
+
+class VsigUnavailable(RuntimeError):
+    """libvsig.so is not built or no HIP device is visible."""
+
+
+class VsigError(RuntimeError):
+    pass
+
+
+class Peak(C.Structure):
+    _fields_ = [("peak", C.c_double), ("index", C.c_int64),
+                ("sum_abs", C.c_double), ("sum_abs2", C.c_double)]
+
+
+P = C.c_void_p
+I32, I64, F32 = C.c_int32, C.c_int64, C.c_float
+
+# name -> (restype, argtypes); every symbol include/vsig.h declares.
+SIGNATURES = {
+    "vsig_version": (C.c_int, []),
+    "vsig_errstr": (C.c_char_p, [C.c_int]),
+    "vsig_init": (C.c_int, [C.c_int, C.POINTER(P)]),
+    "vsig_free": (None, [P]),
+    "vsig_last_error": (C.c_char_p, [P]),
+    "vsig_set_stream": (C.c_int, [P, P]),
+    "vsig_synchronize": (C.c_int, [P]),
+    "vsig_timing_enable": (C.c_int, [P, C.c_int]),
+    "vsig_timing_read": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(I64)]),
+    "vsig_timing_reset": (C.c_int, [P]),
+    "vsig_psd_c64_dev": (C.c_int, [P, P, I64, I64, P, I32, I64, I32, F32, I32, P, I64]),
+    "vsig_psd_c64": (C.c_int, [P, P, I64, P, I32, I64, I32, F32, I32, P, I64]),
+    "vsig_fir_create": (C.c_int, [P, P, I32, I32, C.POINTER(P)]),
+    "vsig_fir_free": (None, [P]),
+    "vsig_fir_exec_dev": (C.c_int, [P, P, I64, P, I64]),
+    "vsig_fir_c64": (C.c_int, [P, P, I64, P, I32, I32, P, I64]),
+    "vsig_xcorr_create": (C.c_int, [P, P, I32, C.POINTER(P)]),
+    "vsig_xcorr_free": (None, [P]),
+    "vsig_xcorr_exec_dev": (C.c_int, [P, P, I64, I32, P, P]),
+    "vsig_correlate_c64_dev": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
+    "vsig_correlate_c64": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
+    "vsig_peak_dev": (C.c_int, [P, I32, P, I64, P]),
+    "vsig_peak": (C.c_int, [P, I32, P, I64, P]),
+}
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library(path: str = LIB_PATH):
+    """Load libvsig.so and declare every entry point; no device needed."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise VsigUnavailable(
+                f"{path} is not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                "(hipcc --offload-arch=gfx950)")
+        lib = C.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+        return lib
+
+
+class Context:
+    """One vsig_ctx on one device (the library's stream state lives here)."""
+
+    def __init__(self, device: int):
+        lib = load_library()
+        h = P()
+        rc = lib.vsig_init(device, C.byref(h))
+        if rc != VSIG_OK:
+            raise VsigUnavailable(f"vsig_init(device={device}) failed: "
+                                  f"{lib.vsig_errstr(rc).decode()}")
+        self.lib, self.h, self.device = lib, h, device
+
+    def check(self, rc: int, what: str):
+        if rc != VSIG_OK:
+            msg = self.lib.vsig_last_error(self.h).decode()
+            err = self.lib.vsig_errstr(rc).decode()
+            if rc == -1:
+                raise ValueError(f"{what}: {err}: {msg}")
+            if rc == -4:
+                raise NotImplementedError(f"{what}: {err}: {msg}")
+            raise VsigError(f"{what}: {err}: {msg}")
+
+    def bind_stream(self):
+        """Enqueue on torch's current stream (so torch events time our kernels)."""
+        s = torch.cuda.current_stream(self.device).cuda_stream
+        self.check(self.lib.vsig_set_stream(self.h, P(s)), "vsig_set_stream")
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.vsig_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+_ctx_tls = threading.local()
+
+
+def get_context(device: int | None = None) -> Context:
+    """Per-thread, per-device context bound to torch's current stream."""
+    if not torch.cuda.is_available():
+        raise VsigUnavailable("vector_amd needs a HIP device (torch.cuda.is_available() is False); "
+                              "there is no CPU fallback")
+    if device is None:
+        device = torch.cuda.current_device()
+    cache = getattr(_ctx_tls, "ctx", None)
+    if cache is None:
+        cache = _ctx_tls.ctx = {}
+    ctx = cache.get(device)
+    if ctx is None:
+        with torch.cuda.device(device):
+            ctx = cache[device] = Context(device)
+    ctx.bind_stream()
+    return ctx

@@ -1,0 +1,260 @@
+// In-LDS Stockham FFT engine for CDNA4 (gfx950), complex fp32.
+//
+// One "frame" of N points is transformed by TF = N / E threads, each holding E
+// complex values in VGPRs.  A pass of radix R does E / R register butterflies
+// per thread; passes exchange data through LDS (padded one float2 per 16 to
+// keep the stride-R scatter writes of the early passes bank-conflict free).
+// The first pass reads its operands straight from the caller's registers (the
+// kernel loads them from HBM with the window / zero-fill fused), the last pass
+// leaves the natural-order spectrum in registers for a fused epilogue
+// (|X|^2 store, filter multiply, correlation peak reduction ...).
+//
+// Index convention (Stockham autosort, natural order in and out):
+//   pass p, radix R, Ns = R_0 * ... * R_{p-1}, butterfly j (0 <= j < N/R):
+//     in : a[j + r*N/R]            r = 0..R-1
+//     tw : a_r *= exp(-2*pi*i * r*(j mod Ns) / (Ns*R))        (p > 0)
+//     out: b[(j/Ns)*Ns*R + (j mod Ns) + r*Ns] = DFT_R(a)_r
+//   thread t of a frame owns butterflies j = t + b*TF, b = 0..E/R-1, and keeps
+//   them in v[b*R + r].  Before pass 0, v[b*R0 + r] must hold x[j + r*N/R0];
+//   after the last pass v[b*RL + r] holds X[j + r*N/RL].
+//
+// Twiddles come from a per-plan table in global memory (L2 resident, built on
+// the host in double precision): for pass p >= 1 the block
+//   tw[off_p + (r-1)*Ns + k] = exp(-2*pi*i * r*k / (Ns*R)),  k < Ns, 1 <= r < R,
+// so the lanes of a wave (consecutive k) read consecutive addresses.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace vsig {
+
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+
+// cos / sin of 2*pi*k/64, k = 0..31 (enough for every in-register radix <= 64).
+constexpr float kCos64[32] = {
+    1.000000000e+00f, 9.951847267e-01f, 9.807852804e-01f, 9.569403357e-01f,
+    9.238795325e-01f, 8.819212643e-01f, 8.314696123e-01f, 7.730104534e-01f,
+    7.071067812e-01f, 6.343932842e-01f, 5.555702330e-01f, 4.713967368e-01f,
+    3.826834324e-01f, 2.902846773e-01f, 1.950903220e-01f, 9.801714033e-02f,
+    0.0f,             -9.801714033e-02f, -1.950903220e-01f, -2.902846773e-01f,
+    -3.826834324e-01f, -4.713967368e-01f, -5.555702330e-01f, -6.343932842e-01f,
+    -7.071067812e-01f, -7.730104534e-01f, -8.314696123e-01f, -8.819212643e-01f,
+    -9.238795325e-01f, -9.569403357e-01f, -9.807852804e-01f, -9.951847267e-01f};
+constexpr float kSin64[32] = {
+    0.0f,             9.801714033e-02f, 1.950903220e-01f, 2.902846773e-01f,
+    3.826834324e-01f, 4.713967368e-01f, 5.555702330e-01f, 6.343932842e-01f,
+    7.071067812e-01f, 7.730104534e-01f, 8.314696123e-01f, 8.819212643e-01f,
+    9.238795325e-01f, 9.569403357e-01f, 9.807852804e-01f, 9.951847267e-01f,
+    1.000000000e+00f, 9.951847267e-01f, 9.807852804e-01f, 9.569403357e-01f,
+    9.238795325e-01f, 8.819212643e-01f, 8.314696123e-01f, 7.730104534e-01f,
+    7.071067812e-01f, 6.343932842e-01f, 5.555702330e-01f, 4.713967368e-01f,
+    3.826834324e-01f, 2.902846773e-01f, 1.950903220e-01f, 9.801714033e-02f};
+
+// b * exp(-2*pi*i*K/M) with compile-time K, M (M <= 64).  Trivial factors
+// (1, -i, and the 45-degree family) are special-cased so they cost no multiply.
+template <int K, int M>
+__device__ __forceinline__ float2 twc(float2 b) {
+  static_assert(M <= 64 && K < M, "in-register twiddle out of range");
+  if constexpr (K == 0) {
+    return b;
+  } else if constexpr (4 * K == M) {            // * (-i)
+    return make_float2(b.y, -b.x);
+  } else if constexpr (8 * K == M) {            // * (1 - i)/sqrt2
+    constexpr float h = 7.071067812e-01f;
+    return make_float2(h * (b.x + b.y), h * (b.y - b.x));
+  } else if constexpr (8 * K == 3 * M) {        // * (-1 - i)/sqrt2
+    constexpr float h = 7.071067812e-01f;
+    return make_float2(h * (b.y - b.x), -h * (b.x + b.y));
+  } else {
+    constexpr int idx = K * (64 / M);
+    constexpr float c = kCos64[idx], s = kSin64[idx];
+    return make_float2(b.x * c + b.y * s, b.y * c - b.x * s);
+  }
+}
+
+// One radix-2 Stockham step inside registers: Ns = 2^P.
+template <int R, int P, int J>
+struct Radix2Step {
+  __device__ __forceinline__ static void run(const float2* a, float2* t) {
+    constexpr int Ns = 1 << P;
+    constexpr int k = J & (Ns - 1);
+    constexpr int o = ((J >> P) << (P + 1)) + k;
+    const float2 x0 = a[J];
+    const float2 x1 = twc<k, 2 * Ns>(a[J + R / 2]);
+    t[o] = cadd(x0, x1);
+    t[o + Ns] = csub(x0, x1);
+    if constexpr (J + 1 < R / 2) Radix2Step<R, P, J + 1>::run(a, t);
+  }
+};
+
+template <int R, int P>
+struct DftPasses {
+  __device__ __forceinline__ static void run(float2* v) {
+    float2 t[R];
+    Radix2Step<R, P, 0>::run(v, t);
+#pragma unroll
+    for (int i = 0; i < R; ++i) v[i] = t[i];
+    if constexpr ((2 << P) < R) DftPasses<R, P + 1>::run(v);
+  }
+};
+
+// In-place natural-order DFT of R = 2^k values held in registers.
+template <int R>
+__device__ __forceinline__ void dft_reg(float2* v) {
+  static_assert((R & (R - 1)) == 0 && R >= 2 && R <= 64, "radix must be a power of two in [2, 64]");
+  DftPasses<R, 0>::run(v);
+}
+
+// ---------------------------------------------------------------------------
+// Plans
+// ---------------------------------------------------------------------------
+template <int N_, int E_, int... Rs>
+struct Plan {
+  static constexpr int N = N_;
+  static constexpr int E = E_;
+  static constexpr int TF = N_ / E_;               // threads per frame
+  static constexpr int NP = sizeof...(Rs);         // number of passes
+  static constexpr int R[NP] = {Rs...};
+  static constexpr int LDS = N_ + N_ / 16;         // padded float2 per frame
+
+  static constexpr int ns(int p) { int s = 1; for (int q = 0; q < p; ++q) s *= R[q]; return s; }
+  static constexpr int twoff(int p) { int o = 0; for (int q = 1; q < p; ++q) o += (R[q] - 1) * ns(q); return o; }
+  static constexpr int twsize() { return twoff(NP); }
+  static constexpr int RL = R[NP - 1];
+  static constexpr bool valid() {
+    int prod = 1;
+    for (int q = 0; q < NP; ++q) { if (E_ % R[q]) return false; prod *= R[q]; }
+    return prod == N_;
+  }
+};
+
+__device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E).
+template <int I> struct IC { static constexpr int value = I; };
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) { f(IC<B>{}); static_for<B + 1, E>(f); }
+}
+
+// stage p: twiddle (p > 0) + register DFT for each of this thread's butterflies
+template <class P, int p>
+__device__ __forceinline__ void fft_stage(float2* v, const float2* __restrict__ tw, int t) {
+  constexpr int R = P::R[p];
+  constexpr int Ns = P::ns(p);
+  constexpr int B = P::E / R;
+#pragma unroll
+  for (int b = 0; b < B; ++b) {
+    if constexpr (p > 0) {
+      const int j = t + b * P::TF;
+      const int k = j & (Ns - 1);
+      const float2* twp = tw + P::twoff(p) + k;
+#pragma unroll
+      for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], twp[(r - 1) * Ns]);
+    }
+    dft_reg<R>(v + b * R);
+  }
+}
+
+// lpad(base + c) for a compile-time c: multiples of 16 become an immediate
+// offset from lpad(base) (lpad(b + 16m) = lpad(b) + 17m), so a pass needs one
+// LDS base address per butterfly instead of one per element.
+template <int C>
+__device__ __forceinline__ int lpad_off(int base, int base_pad) {
+  if constexpr (C % 16 == 0) return base_pad + C + C / 16;
+  else return lpad(base + C);
+}
+
+template <class P, int p>
+__device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
+  constexpr int R = P::R[p];
+  constexpr int Ns = P::ns(p);
+  constexpr int B = P::E / R;
+  static_for<0, B>([&](auto bi) {
+    constexpr int b = decltype(bi)::value;
+    const int j = t + b * P::TF;
+    const int base = (j / Ns) * Ns * R + (j & (Ns - 1));
+    const int bp = lpad(base);
+    static_for<0, R>([&](auto ri) {
+      constexpr int r = decltype(ri)::value;
+      lds[lpad_off<r * Ns>(base, bp)] = v[b * R + r];
+    });
+  });
+}
+
+template <class P, int p>
+__device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
+  constexpr int R = P::R[p];
+  constexpr int B = P::E / R;
+  const int tp = lpad(t);
+  static_for<0, B>([&](auto bi) {
+    constexpr int b = decltype(bi)::value;
+    static_for<0, R>([&](auto ri) {
+      constexpr int r = decltype(ri)::value;
+      v[b * R + r] = lds[lpad_off<b * P::TF + r * (P::N / R)>(t, tp)];
+    });
+  });
+}
+
+template <class P, int p>
+__device__ __forceinline__ void fft_tail(float2* v, float2* lds, const float2* __restrict__ tw, int t) {
+  if constexpr (p < P::NP) {
+    __syncthreads();               // previous readers of lds are done
+    fft_store<P, p - 1>(v, lds, t);
+    __syncthreads();
+    fft_load<P, p>(v, lds, t);
+    fft_stage<P, p>(v, tw, t);
+    fft_tail<P, p + 1>(v, lds, tw, t);
+  }
+}
+
+// Full forward FFT of one frame.  v holds the pass-0 operands on entry and the
+// natural-order spectrum (index j + r*N/RL) on exit.  Contains block barriers:
+// every thread of the block must call it.
+template <class P>
+__device__ __forceinline__ void fft_frame(float2* v, float2* lds, const float2* tw, int t) {
+  static_assert(P::valid(), "invalid FFT plan");
+  // Launder the table pointer: a kernel running two FFTs (overlap-save) would
+  // otherwise have its twiddle loads CSE'd across them and keep every twiddle
+  // of the first FFT live in VGPRs until the second.
+  asm volatile("" : "+s"(tw));
+  fft_stage<P, 0>(v, tw, t);
+  fft_tail<P, 1>(v, lds, tw, t);
+}
+
+// Index helpers for the operand / result layout.
+template <class P>
+__device__ __forceinline__ int in_index(int t, int e) {          // pass-0 operand e of thread t
+  constexpr int R = P::R[0];
+  return t + (e / R) * P::TF + (e % R) * (P::N / R);
+}
+template <class P>
+__device__ __forceinline__ int out_index(int t, int e) {         // result e of thread t
+  constexpr int R = P::RL;
+  return t + (e / R) * P::TF + (e % R) * (P::N / R);
+}
+
+// ---------------------------------------------------------------------------
+// The plans instantiated by the library (N -> elements/thread, radices).
+// Plans used by the overlap-save kernels are palindromic in their first/last
+// radix so the forward FFT's result layout is the inverse FFT's operand layout.
+// ---------------------------------------------------------------------------
+using Plan64 = Plan<64, 8, 8, 8>;
+using Plan128 = Plan<128, 16, 8, 16>;
+using Plan256 = Plan<256, 16, 16, 16>;
+using Plan512 = Plan<512, 16, 8, 8, 8>;
+using Plan1024 = Plan<1024, 32, 32, 32>;
+using Plan2048 = Plan<2048, 32, 8, 32, 8>;
+using Plan4096 = Plan<4096, 16, 16, 16, 16>;
+using Plan8192 = Plan<8192, 32, 16, 32, 16>;
+using Plan16384 = Plan<16384, 16, 16, 4, 16, 16>;
+
+template <class P>
+constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }
+
+}  // namespace vsig

@@ -1,0 +1,380 @@
+// HIP kernels of the vector-signal DSP hot path (gfx950 / CDNA4).
+//
+//   psd_kernel       windowed block FFT -> |X|^2 * scale   (spectrum / create_spectrogram)
+//   fir_os_kernel    overlap-save FIR, decimation folded into the store (filter)
+//   xcorr_os_kernel  overlap-save cross-correlation + fused |c|^2 argmax / sums (correlate)
+//   peak_reduce      double-precision |c| argmax / mean / std over an array (find_correlation_peak)
+//   partial_finalize deterministic reduction of per-block partials
+//   spectrum_prep    FFT of a zero-padded short vector (filter taps / correlation template)
+//
+// All FFT work goes through fft_engine.hpp.  No MFMA: there is no dense
+// contraction on this path; every kernel is HBM- or VALU-bound.
+#include "fft_engine.hpp"
+#include "vsig_kernels.h"
+
+namespace vsig {
+
+// ---------------------------------------------------------------------------
+// spectrum: one frame per TF threads, frames = (n - nperseg) / hop + 1
+// (scipy.signal.spectrogram, scipy/signal/_spectral_py.py:2158-2205, as called
+// at utils.py:281-291).
+// ---------------------------------------------------------------------------
+template <class P>
+__global__ __launch_bounds__(block_threads<P>()) void psd_kernel(
+    const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
+    long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
+    const float2* __restrict__ tw) {
+  constexpr int BT = block_threads<P>();
+  constexpr int FPB = BT / P::TF;
+  __shared__ float2 lds[FPB * P::LDS];
+  const int fl = threadIdx.x / P::TF;
+  const int t = threadIdx.x % P::TF;
+  const long long frame = (long long)blockIdx.x * FPB + fl;
+  const bool active = frame < nframes;
+  const float2* xf = x + (active ? frame * hop * stride : 0);
+
+  float2 v[P::E];
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = in_index<P>(t, e);
+    float2 a = make_float2(0.f, 0.f);
+    if (active && i < nperseg) {
+      const float2 s = xf[(long long)i * stride];
+      const float w = win[i];
+      a = make_float2(s.x * w, s.y * w);
+    }
+    v[e] = a;
+  }
+  fft_frame<P>(v, lds + fl * P::LDS, tw, t);
+  if (!active) return;
+  float* of = out + frame * P::N;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = out_index<P>(t, e);
+    const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+    of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// spectrum_prep: S = FFT_M(zero-padded u) * gain, one frame of M points.
+// conj_in conjugates u first.  Used for the FIR response (H / M) and the
+// correlation template spectrum (P / M).
+// ---------------------------------------------------------------------------
+template <class P>
+__global__ __launch_bounds__(block_threads<P>()) void spectrum_prep(
+    const float2* __restrict__ u, int len, float gain, float2* __restrict__ S,
+    const float2* __restrict__ tw) {
+  constexpr int BT = block_threads<P>();
+  __shared__ float2 lds[(BT / P::TF) * P::LDS];
+  const int fl = threadIdx.x / P::TF;
+  const int t = threadIdx.x % P::TF;
+  float2 v[P::E];
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = in_index<P>(t, e);
+    v[e] = (fl == 0 && i < len) ? u[i] : make_float2(0.f, 0.f);
+  }
+  fft_frame<P>(v, lds + fl * P::LDS, tw, t);
+  if (fl != 0) return;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = out_index<P>(t, e);
+    S[i] = make_float2(v[e].x * gain, v[e].y * gain);
+  }
+}
+
+// Pass-0 operands of an overlap-save segment x[s0 .. s0 + N) with zero fill
+// outside [0, n).  The block-uniform base keeps the address in SGPRs; interior
+// segments (the common case) skip the per-element bounds test.
+template <class P>
+__device__ __forceinline__ void load_segment(float2* v, const float2* __restrict__ x,
+                                             long long s0, long long n, int t) {
+  const float2* base = x + s0;
+  if (s0 >= 0 && s0 + P::N <= n) {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = base[in_index<P>(t, e)];
+  } else {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = in_index<P>(t, e);
+      const long long xi = s0 + i;
+      v[e] = (xi >= 0 && xi < n) ? base[i] : make_float2(0.f, 0.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FIR, overlap-save.  Block b produces outputs g in [b*hop, b*hop + hop) of
+//   y[g] = sum_{m < ntaps} h[m] x[g - m]   (x = 0 outside [0, n))
+// i.e. np.convolve(x, h, 'full')[:n]; only g % decim == 0 is stored, at g/decim.
+// The segment x[b*hop - (ntaps-1) .. + M) is FFT'd, multiplied by Hs = FFT(h)/M
+// and inverse-transformed (conj trick), all in LDS / registers.
+// ---------------------------------------------------------------------------
+template <class P>
+__global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
+    const float2* __restrict__ x, long long n, const float2* __restrict__ Hs, int ntaps,
+    long long hop, int decim, float2* __restrict__ y, long long nblocks,
+    const float2* __restrict__ tw) {
+  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+  constexpr int BT = block_threads<P>();
+  static_assert(BT == P::TF, "one frame per block");
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  const long long b = blockIdx.x;
+  if (b >= nblocks) return;  // uniform per block
+  const long long s0 = b * hop - (ntaps - 1);
+
+  float2 v[P::E];
+  load_segment<P>(v, x, s0, n, t);
+  fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+  fft_frame<P>(v, lds, tw, t);
+  const int lo = ntaps - 1;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = out_index<P>(t, e) - lo;
+    const long long g = b * hop + i;
+    if (i >= 0 && i < hop && g < n && (decim == 1 || g % decim == 0))
+      y[decim == 1 ? g : g / decim] = cconj(v[e]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Block partial of a |c| reduction: max |c|^2 (lowest index on ties),
+// sum |c|, sum |c|^2.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void better(float& m, long long& i, float m2, long long i2) {
+  if (m2 > m || (m2 == m && i2 < i)) { m = m2; i = i2; }
+}
+__device__ __forceinline__ void betterd(double& m, long long& i, double m2, long long i2) {
+  if (m2 > m || (m2 == m && i2 < i)) { m = m2; i = i2; }
+}
+
+template <int BT>
+__device__ __forceinline__ void block_partial(double m, long long mi, double s1, double s2,
+                                              PeakPartial* out) {
+  // wave reduce (64 lanes)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double om = __shfl_xor(m, off);
+    const long long oi = __shfl_xor(mi, off);
+    betterd(m, mi, om, oi);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  constexpr int NW = BT / 64;
+  __shared__ double sm[NW], ss1[NW], ss2[NW];
+  __shared__ long long si[NW];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) { sm[w] = m; si[w] = mi; ss1[w] = s1; ss2[w] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < NW; ++q) { betterd(m, mi, sm[q], si[q]); s1 += ss1[q]; s2 += ss2[q]; }
+    out->max2 = m; out->idx = mi; out->sum_abs = s1; out->sum_abs2 = s2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Cross-correlation, overlap-save:  c[o] = sum_{k<L} s[o - off + k] * conj(p[k]),
+// o in [0, nout).  off = 0 -> np.correlate 'valid'; off = L-1 -> 'full'.
+// Block b: outputs [b*hop, b*hop + hop), hop <= M - L + 1.
+// Epilogue: optional store of c (or of conj(c) at nout-1-o, for the swapped
+// argument order of np.correlate), and the block's |c| partial.
+// ---------------------------------------------------------------------------
+template <class P>
+__global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
+    const float2* __restrict__ s, long long n, const float2* __restrict__ Ps, long long off,
+    long long nout, long long hop, float2* __restrict__ c, int store_mode,
+    PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw) {
+  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+  constexpr int BT = block_threads<P>();
+  static_assert(BT == P::TF, "one frame per block");
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  const long long b = blockIdx.x;
+  if (b >= nblocks) return;
+  const long long s0 = b * hop - off;
+
+  float2 v[P::E];
+  load_segment<P>(v, s, s0, n, t);
+  fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+  fft_frame<P>(v, lds, tw, t);
+
+  float m = -1.f;
+  long long mi = 0x7fffffffffffffffLL;
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = out_index<P>(t, e);
+    const long long o = b * hop + i;
+    if (i < hop && o < nout) {
+      const float2 cv = cconj(v[e]);
+      const float a2 = cv.x * cv.x + cv.y * cv.y;
+      better(m, mi, a2, o);
+      s1 += sqrtf(a2);
+      s2 += a2;
+      if (store_mode == 1) c[o] = cv;
+      else if (store_mode == 2) c[nout - 1 - o] = cconj(cv);
+    }
+  }
+  if (partials) block_partial<BT>((double)m, mi, (double)s1, (double)s2, partials + b);
+}
+
+// ---------------------------------------------------------------------------
+// |c| reduction over an array in double precision (find_correlation_peak,
+// utils.py:1321-1334): |c| = hypot(re, im) like np.abs, first max wins.
+// T = double2 (complex128), float2 (complex64), double, float.
+// ---------------------------------------------------------------------------
+template <class T> __device__ __forceinline__ double absval(const T* p, long long i);
+template <> __device__ __forceinline__ double absval<double2>(const double2* p, long long i) {
+  const double2 v = p[i]; return hypot(v.x, v.y);
+}
+template <> __device__ __forceinline__ double absval<float2>(const float2* p, long long i) {
+  const float2 v = p[i]; return (double)hypotf(v.x, v.y);
+}
+template <> __device__ __forceinline__ double absval<double>(const double* p, long long i) { return fabs(p[i]); }
+template <> __device__ __forceinline__ double absval<float>(const float* p, long long i) { return (double)fabsf(p[i]); }
+
+template <class T>
+__global__ __launch_bounds__(256) void peak_reduce(const T* __restrict__ a, long long n,
+                                                   PeakPartial* __restrict__ partials) {
+  double m = -1.0, s1 = 0.0, s2 = 0.0;
+  long long mi = 0x7fffffffffffffffLL;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const double v = absval<T>(a, i);
+    betterd(m, mi, v, i);
+    s1 += v;
+    s2 += v * v;
+  }
+  block_partial<256>(m, mi, s1, s2, partials + blockIdx.x);
+}
+
+// Fixed-order reduction of nparts partials into out[0]; sqrt_max converts a
+// max |c|^2 into max |c|.
+__global__ __launch_bounds__(1024) void partial_finalize(const PeakPartial* __restrict__ parts,
+                                                         long long nparts, int sqrt_max,
+                                                         PeakPartial* __restrict__ out) {
+  double m = -1.0, s1 = 0.0, s2 = 0.0;
+  long long mi = 0x7fffffffffffffffLL;
+  for (long long i = threadIdx.x; i < nparts; i += 1024) {
+    const PeakPartial p = parts[i];
+    betterd(m, mi, p.max2, p.idx);
+    s1 += p.sum_abs;
+    s2 += p.sum_abs2;
+  }
+  __shared__ PeakPartial tmp[1];
+  block_partial<1024>(m, mi, s1, s2, tmp);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    PeakPartial r = tmp[0];
+    if (sqrt_max) r.max2 = sqrt(r.max2);
+    *out = r;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers (called from vsig_api.hip), dispatching N to plans.
+// ---------------------------------------------------------------------------
+#define VSIG_PLAN_SWITCH(N, BODY)                          \
+  switch (N) {                                             \
+    case 64: { using PL = Plan64; BODY; } break;           \
+    case 128: { using PL = Plan128; BODY; } break;         \
+    case 256: { using PL = Plan256; BODY; } break;         \
+    case 512: { using PL = Plan512; BODY; } break;         \
+    case 1024: { using PL = Plan1024; BODY; } break;       \
+    case 2048: { using PL = Plan2048; BODY; } break;       \
+    case 4096: { using PL = Plan4096; BODY; } break;       \
+    case 8192: { using PL = Plan8192; BODY; } break;       \
+    case 16384: { using PL = Plan16384; BODY; } break;     \
+    default: return hipErrorInvalidValue;                  \
+  }
+
+hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
+                      long long hop, float scale, float* out, long long nframes, int shift,
+                      const float2* tw, hipStream_t st) {
+  if (nframes <= 0) return hipSuccess;
+  VSIG_PLAN_SWITCH(N, {
+    constexpr int BT = block_threads<PL>();
+    constexpr int FPB = BT / PL::TF;
+    const long long grid = (nframes + FPB - 1) / FPB;
+    hipLaunchKernelGGL(psd_kernel<PL>, dim3((unsigned)grid), dim3(BT), 0, st, x, stride, win,
+                       nperseg, hop, scale, out, nframes, shift, tw);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
+                                const float2* tw, hipStream_t st) {
+  VSIG_PLAN_SWITCH(N, {
+    hipLaunchKernelGGL(spectrum_prep<PL>, dim3(1), dim3(block_threads<PL>()), 0, st, u, len,
+                       gain, S, tw);
+  });
+  return hipGetLastError();
+}
+
+// Only plans with one frame per block can run the overlap-save kernels.
+#define VSIG_OS_SWITCH(N, BODY)                            \
+  switch (N) {                                             \
+    case 4096: { using PL = Plan4096; BODY; } break;       \
+    case 8192: { using PL = Plan8192; BODY; } break;       \
+    case 16384: { using PL = Plan16384; BODY; } break;     \
+    default: return hipErrorInvalidValue;                  \
+  }
+
+hipError_t launch_fir_os(int M, const float2* x, long long n, const float2* Hs, int ntaps,
+                         long long hop, int decim, float2* y, const float2* tw, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const long long nblocks = (n + hop - 1) / hop;
+  VSIG_OS_SWITCH(M, {
+    hipLaunchKernelGGL(fir_os_kernel<PL>, dim3((unsigned)nblocks), dim3(block_threads<PL>()), 0,
+                       st, x, n, Hs, ntaps, hop, decim, y, nblocks, tw);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
+                           long long nout, long long hop, float2* c, int store_mode,
+                           PeakPartial* partials, const float2* tw, hipStream_t st) {
+  if (nout <= 0) return hipSuccess;
+  const long long nblocks = (nout + hop - 1) / hop;
+  VSIG_OS_SWITCH(M, {
+    hipLaunchKernelGGL(xcorr_os_kernel<PL>, dim3((unsigned)nblocks), dim3(block_threads<PL>()),
+                       0, st, s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
+                              int nparts, hipStream_t st) {
+  switch (dtype) {
+    case VSIG_C128: hipLaunchKernelGGL(peak_reduce<double2>, dim3(nparts), dim3(256), 0, st, (const double2*)a, n, partials); break;
+    case VSIG_C64: hipLaunchKernelGGL(peak_reduce<float2>, dim3(nparts), dim3(256), 0, st, (const float2*)a, n, partials); break;
+    case VSIG_F64: hipLaunchKernelGGL(peak_reduce<double>, dim3(nparts), dim3(256), 0, st, (const double*)a, n, partials); break;
+    case VSIG_F32: hipLaunchKernelGGL(peak_reduce<float>, dim3(nparts), dim3(256), 0, st, (const float*)a, n, partials); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
+                                   PeakPartial* out, hipStream_t st) {
+  hipLaunchKernelGGL(partial_finalize, dim3(1), dim3(1024), 0, st, parts, nparts, sqrt_max, out);
+  return hipGetLastError();
+}
+
+}  // namespace vsig
+
+namespace vsig {
+hipError_t plan_info(int N, int* radices, int* npasses) {
+  VSIG_PLAN_SWITCH(N, {
+    *npasses = PL::NP;
+    for (int q = 0; q < PL::NP; ++q) radices[q] = PL::R[q];
+  });
+  return hipSuccess;
+}
+}  // namespace vsig

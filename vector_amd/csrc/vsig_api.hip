@@ -1,0 +1,501 @@
+// C-ABI layer of libvsig.so (declared in include/vsig.h): contexts, plans
+// (twiddle tables, filter / template spectra), launch geometry, host staging.
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/vsig.h"
+#include "vsig_kernels.h"
+
+using vsig::PeakPartial;
+
+struct TimingRec {
+  std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+};
+
+struct vsig_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  std::map<int, float2*> tw;             // FFT size -> device twiddle table
+  PeakPartial* partials = nullptr;       // per-block partials
+  long long npartials = 0;
+  PeakPartial* result = nullptr;         // scratch device result
+  void* stage[3] = {nullptr, nullptr, nullptr};  // host-API device staging
+  size_t stage_bytes[3] = {0, 0, 0};
+  std::string err;
+  bool timing = false;
+  std::map<std::string, TimingRec> timers;
+};
+
+struct vsig_fir {
+  vsig_ctx* ctx;
+  int ntaps, decim, M;
+  long long hop;
+  float2* Hs;
+};
+
+struct vsig_xcorr {
+  vsig_ctx* ctx;
+  int L, M;
+  float2* Ps;
+};
+
+namespace {
+
+int fail(vsig_ctx* c, int code, const std::string& msg) {
+  if (c) c->err = msg;
+  return code;
+}
+
+#define HIPCHK(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t e_ = (expr);                                                            \
+    if (e_ != hipSuccess)                                                              \
+      return fail(ctx, e_ == hipErrorOutOfMemory ? VSIG_E_NOMEM : VSIG_E_HIP,          \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+  } while (0)
+
+// Twiddle table of the plan for N (see fft_engine.hpp):
+// tw[off_p + (r-1)*Ns + k] = exp(-2 pi i r k / (Ns R)), passes p >= 1.
+int get_twiddles(vsig_ctx* c, int N, const float2** out) {
+  auto it = c->tw.find(N);
+  if (it != c->tw.end()) { *out = it->second; return VSIG_OK; }
+  int R[16], np = 0;
+  if (vsig::plan_info(N, R, &np) != hipSuccess)
+    return fail(c, VSIG_E_UNSUPPORTED, "FFT size " + std::to_string(N) + " not supported");
+  std::vector<float2> h;
+  int Ns = R[0];
+  for (int p = 1; p < np; ++p) {
+    for (int r = 1; r < R[p]; ++r)
+      for (int k = 0; k < Ns; ++k) {
+        const double a = -2.0 * M_PI * (double)r * (double)k / ((double)Ns * R[p]);
+        h.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+      }
+    Ns *= R[p];
+  }
+  if (h.empty()) h.push_back(make_float2(1.f, 0.f));
+  float2* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, h.size() * sizeof(float2)));
+  HIPCHK(c, hipMemcpy(d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice));
+  c->tw[N] = d;
+  *out = d;
+  return VSIG_OK;
+}
+
+int ensure_partials(vsig_ctx* c, long long n) {
+  if (n <= c->npartials) return VSIG_OK;
+  if (c->partials) (void)hipFree(c->partials);
+  c->partials = nullptr;
+  c->npartials = 0;
+  long long cap = n < 4096 ? 4096 : n + n / 4;
+  HIPCHK(c, hipMalloc(&c->partials, cap * sizeof(PeakPartial)));
+  c->npartials = cap;
+  return VSIG_OK;
+}
+
+int ensure_stage(vsig_ctx* c, int i, size_t bytes) {
+  if (bytes <= c->stage_bytes[i]) return VSIG_OK;
+  if (c->stage[i]) (void)hipFree(c->stage[i]);
+  c->stage[i] = nullptr;
+  c->stage_bytes[i] = 0;
+  HIPCHK(c, hipMalloc(&c->stage[i], bytes));
+  c->stage_bytes[i] = bytes;
+  return VSIG_OK;
+}
+
+// Event pair around one kernel launch (only when timing is on).
+struct Timed {
+  vsig_ctx* c;
+  hipEvent_t b = nullptr, e = nullptr;
+  const char* name;
+  Timed(vsig_ctx* c_, const char* n) : c(c_), name(n) {
+    if (!c->timing) return;
+    if (hipEventCreate(&b) != hipSuccess || hipEventCreate(&e) != hipSuccess) { b = e = nullptr; return; }
+    (void)hipEventRecord(b, c->stream);
+  }
+  ~Timed() {
+    if (!b) return;
+    (void)hipEventRecord(e, c->stream);
+    c->timers[name].ev.emplace_back(b, e);
+  }
+};
+
+bool pow2_in(long long v, long long lo, long long hi) {
+  return v >= lo && v <= hi && (v & (v - 1)) == 0;
+}
+
+int os_size_fir(int ntaps) {
+  if (ntaps <= 512) return 4096;
+  if (ntaps <= 2048) return 8192;
+  if (ntaps <= 8192) return 16384;
+  return 0;
+}
+int os_size_xcorr(int L) {
+  if (L <= 1024) return 4096;
+  if (L <= 2048) return 8192;
+  if (L <= 8192) return 16384;
+  return 0;
+}
+
+// FFT_M(zero-padded u[0..len)) * gain into a new device buffer.
+int make_spectrum(vsig_ctx* c, const float2* u_dev, int len, int M, float2** out) {
+  const float2* tw;
+  int rc = get_twiddles(c, M, &tw);
+  if (rc) return rc;
+  float2* S = nullptr;
+  HIPCHK(c, hipMalloc(&S, (size_t)M * sizeof(float2)));
+  hipError_t e = vsig::launch_spectrum_prep(M, u_dev, len, 1.0f / (float)M, S, tw, c->stream);
+  if (e != hipSuccess) { (void)hipFree(S); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
+  *out = S;
+  return VSIG_OK;
+}
+
+int finalize_peak(vsig_ctx* c, long long nparts, int sqrt_max, vsig_peak_t* peak_dev) {
+  PeakPartial* dst = peak_dev ? reinterpret_cast<PeakPartial*>(peak_dev) : c->result;
+  HIPCHK(c, vsig::launch_partial_finalize(c->partials, nparts, sqrt_max, dst, c->stream));
+  return VSIG_OK;
+}
+
+// Shared by the plan-based and the general correlation paths.
+int run_xcorr(vsig_ctx* c, int M, const float2* Ps, int L, const float2* s, long long n,
+              long long off, long long nout, int store_mode, void* cout, vsig_peak_t* peak_dev) {
+  const long long hop = (long long)M - L + 1;
+  const long long nblocks = nout > 0 ? (nout + hop - 1) / hop : 0;
+  if (nout <= 0) return fail(c, VSIG_E_INVALID, "empty correlation output");
+  int rc = ensure_partials(c, nblocks);
+  if (rc) return rc;
+  const float2* tw;
+  rc = get_twiddles(c, M, &tw);
+  if (rc) return rc;
+  {
+    Timed t(c, "xcorr");
+    HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
+                                    c->partials, tw, c->stream));
+  }
+  return finalize_peak(c, nblocks, 1, peak_dev);
+}
+
+}  // namespace
+
+extern "C" {
+
+int vsig_version(void) { return 1; }
+
+const char* vsig_errstr(int s) {
+  switch (s) {
+    case VSIG_OK: return "ok";
+    case VSIG_E_INVALID: return "invalid argument";
+    case VSIG_E_HIP: return "HIP runtime error";
+    case VSIG_E_NOMEM: return "device out of memory";
+    case VSIG_E_UNSUPPORTED: return "unsupported size";
+    case VSIG_E_NODEVICE: return "no HIP device";
+    default: return "unknown status";
+  }
+}
+
+int vsig_init(int device, vsig_ctx** out) {
+  if (!out) return VSIG_E_INVALID;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return VSIG_E_NODEVICE;
+  if (device < 0 || device >= ndev) return VSIG_E_INVALID;
+  if (hipSetDevice(device) != hipSuccess) return VSIG_E_HIP;
+  vsig_ctx* c = new vsig_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return VSIG_E_HIP; }
+  c->stream = c->own;
+  if (hipMalloc(&c->result, sizeof(PeakPartial)) != hipSuccess) { vsig_free(c); return VSIG_E_NOMEM; }
+  *out = c;
+  return VSIG_OK;
+}
+
+int vsig_timing_reset(vsig_ctx* c) {
+  if (!c) return VSIG_E_INVALID;
+  for (auto& kv : c->timers)
+    for (auto& p : kv.second.ev) { (void)hipEventDestroy(p.first); (void)hipEventDestroy(p.second); }
+  c->timers.clear();
+  return VSIG_OK;
+}
+
+void vsig_free(vsig_ctx* c) {
+  if (!c) return;
+  (void)hipSetDevice(c->device);
+  (void)hipDeviceSynchronize();
+  vsig_timing_reset(c);
+  for (auto& kv : c->tw) (void)hipFree(kv.second);
+  if (c->partials) (void)hipFree(c->partials);
+  if (c->result) (void)hipFree(c->result);
+  for (int i = 0; i < 3; ++i) if (c->stage[i]) (void)hipFree(c->stage[i]);
+  if (c->own) (void)hipStreamDestroy(c->own);
+  delete c;
+}
+
+const char* vsig_last_error(const vsig_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int vsig_set_stream(vsig_ctx* c, void* s) {
+  if (!c) return VSIG_E_INVALID;
+  c->stream = s ? (hipStream_t)s : c->own;
+  return VSIG_OK;
+}
+
+int vsig_synchronize(vsig_ctx* c) {
+  if (!c) return VSIG_E_INVALID;
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+int vsig_timing_enable(vsig_ctx* c, int on) {
+  if (!c) return VSIG_E_INVALID;
+  c->timing = on != 0;
+  return VSIG_OK;
+}
+
+int vsig_timing_read(vsig_ctx* c, const char* kernel, double* total_ms, int64_t* launches) {
+  if (!c || !kernel || !total_ms || !launches) return VSIG_E_INVALID;
+  *total_ms = 0.0;
+  *launches = 0;
+  auto it = c->timers.find(kernel);
+  if (it == c->timers.end()) return VSIG_OK;
+  for (auto& p : it->second.ev) {
+    HIPCHK(c, hipEventSynchronize(p.second));
+    float ms = 0.f;
+    HIPCHK(c, hipEventElapsedTime(&ms, p.first, p.second));
+    *total_ms += ms;
+    *launches += 1;
+  }
+  return VSIG_OK;
+}
+
+// ---------------------------------------------------------------- spectrum
+int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, const float* win,
+                     int32_t nperseg, int64_t hop, int32_t nfft, float scale, int32_t shift,
+                     float* sxx, int64_t nframes) {
+  if (!c || !x || !win || !sxx) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (stride < 1) return fail(c, VSIG_E_INVALID, "stride must be >= 1");
+  if (!pow2_in(nfft, 64, 16384))
+    return fail(c, VSIG_E_UNSUPPORTED, "nfft must be a power of two in [64, 16384]");
+  if (nperseg < 1 || nperseg > nfft || hop < 1 || n < nperseg)
+    return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
+  if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
+  const float2* tw;
+  int rc = get_twiddles(c, nfft, &tw);
+  if (rc) return rc;
+  Timed t(c, "psd");
+  HIPCHK(c, vsig::launch_psd(nfft, (const float2*)x, stride, win, nperseg, hop, scale, sxx, nframes,
+                             shift, tw, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_psd_c64(vsig_ctx* c, const void* x, int64_t n, const float* win, int32_t nperseg,
+                 int64_t hop, int32_t nfft, float scale, int32_t shift, float* sxx,
+                 int64_t nframes) {
+  if (!c || !x || !win || !sxx) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < nperseg || nperseg < 1 || hop < 1) return fail(c, VSIG_E_INVALID, "bad sizes");
+  const size_t bx = (size_t)n * 8, bw = (size_t)nperseg * 4, bo = (size_t)nframes * nfft * 4;
+  int rc;
+  if ((rc = ensure_stage(c, 0, bx)) || (rc = ensure_stage(c, 1, bw)) || (rc = ensure_stage(c, 2, bo)))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->stage[0], x, bx, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->stage[1], win, bw, hipMemcpyHostToDevice, c->stream));
+  rc = vsig_psd_c64_dev(c, c->stage[0], n, 1, (const float*)c->stage[1], nperseg, hop, nfft, scale,
+                        shift, (float*)c->stage[2], nframes);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(sxx, c->stage[2], bo, hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+// ---------------------------------------------------------------- FIR
+int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim, vsig_fir** out) {
+  if (!c || !taps || !out) return fail(c, VSIG_E_INVALID, "null pointer");
+  *out = nullptr;
+  if (ntaps < 1 || decim < 1) return fail(c, VSIG_E_INVALID, "ntaps and decim must be >= 1");
+  const int M = os_size_fir(ntaps);
+  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "ntaps > 8192");
+  long long hop = ((long long)M - (ntaps - 1)) / decim * decim;
+  if (hop < 1) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
+  float2* hd = nullptr;
+  HIPCHK(c, hipMalloc(&hd, (size_t)ntaps * sizeof(float2)));
+  hipError_t e = hipMemcpyAsync(hd, taps, (size_t)ntaps * sizeof(float2), hipMemcpyHostToDevice, c->stream);
+  if (e != hipSuccess) { (void)hipFree(hd); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
+  float2* Hs = nullptr;
+  int rc = make_spectrum(c, hd, ntaps, M, &Hs);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(hd);
+  if (rc) return rc;
+  *out = new vsig_fir{c, ntaps, decim, M, hop, Hs};
+  return VSIG_OK;
+}
+
+void vsig_fir_free(vsig_fir* f) {
+  if (!f) return;
+  (void)hipStreamSynchronize(f->ctx->stream);
+  (void)hipFree(f->Hs);
+  delete f;
+}
+
+int vsig_fir_exec_dev(vsig_fir* f, const void* x, int64_t n, void* y, int64_t ny) {
+  if (!f) return VSIG_E_INVALID;
+  vsig_ctx* c = f->ctx;
+  if (!x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
+  const float2* tw;
+  int rc = get_twiddles(c, f->M, &tw);
+  if (rc) return rc;
+  Timed t(c, "fir");
+  HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, n, f->Hs, f->ntaps, f->hop, f->decim,
+                                (float2*)y, tw, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_fir_c64(vsig_ctx* c, const void* x, int64_t n, const float* taps, int32_t ntaps,
+                 int32_t decim, void* y, int64_t ny) {
+  if (!c || !x || !taps || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (ntaps < 1) return fail(c, VSIG_E_INVALID, "ntaps must be >= 1");
+  std::vector<float2> tc(ntaps);
+  for (int i = 0; i < ntaps; ++i) tc[i] = make_float2(taps[i], 0.f);
+  vsig_fir* f = nullptr;
+  int rc = vsig_fir_create(c, tc.data(), ntaps, decim, &f);
+  if (rc) return rc;
+  const size_t bx = (size_t)n * 8, by = (size_t)ny * 8;
+  if ((rc = ensure_stage(c, 0, bx)) || (rc = ensure_stage(c, 1, by))) { vsig_fir_free(f); return rc; }
+  hipError_t e = hipMemcpyAsync(c->stage[0], x, bx, hipMemcpyHostToDevice, c->stream);
+  if (e == hipSuccess) {
+    rc = vsig_fir_exec_dev(f, c->stage[0], n, c->stage[1], ny);
+    if (!rc) e = hipMemcpyAsync(y, c->stage[1], by, hipMemcpyDeviceToHost, c->stream);
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  vsig_fir_free(f);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(c, VSIG_E_HIP, hipGetErrorString(e));
+  return VSIG_OK;
+}
+
+// ---------------------------------------------------------------- correlation
+int vsig_xcorr_create(vsig_ctx* c, const void* tmpl, int32_t L, vsig_xcorr** out) {
+  if (!c || !tmpl || !out) return fail(c, VSIG_E_INVALID, "null pointer");
+  *out = nullptr;
+  if (L < 1) return fail(c, VSIG_E_INVALID, "template length must be >= 1");
+  const int M = os_size_xcorr(L);
+  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "template longer than 8192");
+  float2* td = nullptr;
+  HIPCHK(c, hipMalloc(&td, (size_t)L * sizeof(float2)));
+  hipError_t e = hipMemcpyAsync(td, tmpl, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, c->stream);
+  if (e != hipSuccess) { (void)hipFree(td); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
+  float2* Ps = nullptr;
+  int rc = make_spectrum(c, td, L, M, &Ps);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(td);
+  if (rc) return rc;
+  *out = new vsig_xcorr{c, L, M, Ps};
+  return VSIG_OK;
+}
+
+void vsig_xcorr_free(vsig_xcorr* x) {
+  if (!x) return;
+  (void)hipStreamSynchronize(x->ctx->stream);
+  (void)hipFree(x->Ps);
+  delete x;
+}
+
+int vsig_xcorr_exec_dev(vsig_xcorr* x, const void* s, int64_t n, int32_t mode, void* cout,
+                        vsig_peak_t* peak_dev) {
+  if (!x) return VSIG_E_INVALID;
+  vsig_ctx* c = x->ctx;
+  if (!s) return fail(c, VSIG_E_INVALID, "null pointer");
+  long long off, nout;
+  if (mode == VSIG_MODE_VALID) { off = 0; nout = n - x->L + 1; }
+  else if (mode == VSIG_MODE_FULL) { off = x->L - 1; nout = n + x->L - 1; }
+  else return fail(c, VSIG_E_INVALID, "streaming correlation supports VALID and FULL");
+  if (nout < 1) return fail(c, VSIG_E_INVALID, "stream shorter than the template");
+  return run_xcorr(c, x->M, x->Ps, x->L, (const float2*)s, n, off, nout, cout ? 1 : 0, cout,
+                   peak_dev);
+}
+
+int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
+                           int32_t mode, void* cout, vsig_peak_t* peak_dev) {
+  if (!c || !a || !v) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (na < 1 || nv < 1) return fail(c, VSIG_E_INVALID, "empty input");  // numeric.py:865-868
+  const long long nmin = na < nv ? na : nv, nmax = na < nv ? nv : na;
+  long long F, nout;  // start index into the 'full' correlation, output length
+  if (mode == VSIG_MODE_FULL) { F = 0; nout = na + nv - 1; }
+  else if (mode == VSIG_MODE_VALID) { F = nmin - 1; nout = nmax - nmin + 1; }
+  else if (mode == VSIG_MODE_SAME) { F = na >= nv ? nmin - 1 - nmin / 2 : nmin / 2; nout = nmax; }
+  else return fail(c, VSIG_E_INVALID, "mode must be VALID, FULL or SAME");
+  const bool swap = nv > na;  // template must be the shorter operand
+  const float2* tmpl = (const float2*)(swap ? a : v);
+  const float2* strm = (const float2*)(swap ? v : a);
+  const int L = (int)nmin;
+  const int M = os_size_xcorr(L);
+  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "shorter operand longer than 8192");
+  float2* Ps = nullptr;
+  int rc = make_spectrum(c, tmpl, L, M, &Ps);
+  if (rc) return rc;
+  // c[o] = full[F + o]; full[i] = sum_k a[i-(nv-1)+k] conj(v[k]).
+  // Not swapped: kernel offset off = (L-1) - F.  Swapped: compute the
+  // correlation of v by a and store conj() reversed, off' = F + nout - nv.
+  const long long off = swap ? F + nout - nv : (L - 1) - F;
+  rc = run_xcorr(c, M, Ps, L, strm, nmax, off, nout, cout ? (swap ? 2 : 1) : 0, cout, peak_dev);
+  (void)hipStreamSynchronize(c->stream);
+  (void)hipFree(Ps);
+  return rc;
+}
+
+int vsig_correlate_c64(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
+                       int32_t mode, void* cout, vsig_peak_t* peak) {
+  if (!c || !a || !v) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (na < 1 || nv < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  const long long nmin = na < nv ? na : nv, nmax = na < nv ? nv : na;
+  const long long nout = mode == VSIG_MODE_FULL ? na + nv - 1
+                       : mode == VSIG_MODE_VALID ? nmax - nmin + 1 : nmax;
+  int rc;
+  if ((rc = ensure_stage(c, 0, (size_t)na * 8)) || (rc = ensure_stage(c, 1, (size_t)nv * 8)) ||
+      (cout && (rc = ensure_stage(c, 2, (size_t)nout * 8))))
+    return rc;
+  HIPCHK(c, hipMemcpyAsync(c->stage[0], a, (size_t)na * 8, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->stage[1], v, (size_t)nv * 8, hipMemcpyHostToDevice, c->stream));
+  rc = vsig_correlate_c64_dev(c, c->stage[0], na, c->stage[1], nv, mode, cout ? c->stage[2] : nullptr,
+                              nullptr);
+  if (rc) return rc;
+  if (cout) HIPCHK(c, hipMemcpyAsync(cout, c->stage[2], (size_t)nout * 8, hipMemcpyDeviceToHost, c->stream));
+  if (peak) HIPCHK(c, hipMemcpyAsync(peak, c->result, sizeof(vsig_peak_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+// ---------------------------------------------------------------- peak
+int vsig_peak_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev) {
+  if (!c || !a) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");  // np.argmax of empty raises
+  if (dtype < VSIG_DTYPE_C128 || dtype > VSIG_DTYPE_F32) return fail(c, VSIG_E_INVALID, "dtype");
+  long long nparts = (n + 255) / 256;
+  if (nparts > 2048) nparts = 2048;
+  int rc = ensure_partials(c, nparts);
+  if (rc) return rc;
+  {
+    Timed t(c, "peak");
+    HIPCHK(c, vsig::launch_peak_reduce(dtype, a, n, c->partials, (int)nparts, c->stream));
+  }
+  return finalize_peak(c, nparts, 0, peak_dev);
+}
+
+int vsig_peak(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak) {
+  if (!c || !a || !peak) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  const size_t es = dtype == VSIG_DTYPE_C128 ? 16 : (dtype == VSIG_DTYPE_F32 ? 4 : 8);
+  int rc = ensure_stage(c, 0, (size_t)n * es);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(c->stage[0], a, (size_t)n * es, hipMemcpyHostToDevice, c->stream));
+  rc = vsig_peak_dev(c, dtype, c->stage[0], n, nullptr);
+  if (rc) return rc;
+  HIPCHK(c, hipMemcpyAsync(peak, c->result, sizeof(vsig_peak_t), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+}  // extern "C"

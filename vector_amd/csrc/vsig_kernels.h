@@ -1,0 +1,34 @@
+// Internal interface between the C-ABI layer (vsig_api.hip) and the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace vsig {
+
+enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
+
+// One block's |c| reduction partial (also the layout of the final result).
+struct PeakPartial {
+  double max2;       // max |c|^2 (kernels on |c|^2) or max |c| (peak_reduce / finalized)
+  long long idx;     // index of the first maximum
+  double sum_abs;    // sum |c|
+  double sum_abs2;   // sum |c|^2
+};
+
+hipError_t plan_info(int N, int* radices, int* npasses);
+
+hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
+                      long long hop, float scale, float* out, long long nframes, int shift,
+                      const float2* tw, hipStream_t st);
+hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
+                                const float2* tw, hipStream_t st);
+hipError_t launch_fir_os(int M, const float2* x, long long n, const float2* Hs, int ntaps,
+                         long long hop, int decim, float2* y, const float2* tw, hipStream_t st);
+hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
+                           long long nout, long long hop, float2* c, int store_mode,
+                           PeakPartial* partials, const float2* tw, hipStream_t st);
+hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
+                              int nparts, hipStream_t st);
+hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
+                                   PeakPartial* out, hipStream_t st);
+
+}  // namespace vsig

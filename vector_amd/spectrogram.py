@@ -1,0 +1,110 @@
+"""create_spectrogram — the reference's adaptive STFT entry point
+(utils.py:161-353) with its STFT core on the MI355X PSD kernel.
+
+The host part is O(1) parameter selection, restated line by line from the
+reference so shapes, windows and fallbacks are identical; the stride
+decimation ``sig[::factor]`` (utils.py:192-195) is folded into the kernel's
+load (device inputs) or into the host->device copy (host inputs), and the
+fftshift of Sxx (utils.py:351) into its store.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from . import dsp
+from ._lib import get_context
+
+__all__ = ["create_spectrogram", "spectrogram_params"]
+
+
+def spectrogram_params(n, sr, max_samples=2_000_000, time_resolution_us=1,
+                       adaptive_resolution=True):
+    """Parameter logic of utils.py:176-276 for a signal of n samples."""
+    if n == 0:
+        raise ValueError("Signal is empty")                          # utils.py:180-181
+    heavy = n > 5_000_000                                            # :184
+    if heavy:
+        max_samples = min(max_samples, 1_000_000)                    # :188
+        time_resolution_us = max(time_resolution_us, 20)             # :189
+    if n > max_samples:                                              # :192-195
+        factor = int(np.ceil(n / max_samples))
+        nsig = (n + factor - 1) // factor
+        fs = sr / factor
+    else:
+        factor, nsig, fs = 1, n, sr
+    dur_us = nsig / fs * 1e6                                         # :203
+    if adaptive_resolution:                                          # :206-234
+        if dur_us <= 50:
+            base, tres, frf = max(32, min(nsig // 12, 128)), min(time_resolution_us, dur_us / 10), 1.2
+        elif dur_us <= 500:
+            base, tres, frf = max(64, min(nsig // 10, 256)), min(time_resolution_us, dur_us / 20), 1.2
+        elif dur_us <= 5000:
+            base, tres, frf = max(128, min(nsig // 8, 512)), min(time_resolution_us, 10), 1.5
+        else:
+            base, tres, frf = max(256, min(nsig // 6, 1024)), min(time_resolution_us, 20), 1.5
+            if heavy:
+                base, tres, frf = min(base, 512), max(tres, 50), 1.2
+    else:
+        base, tres, frf = max(128, min(nsig // 8, 512)), time_resolution_us, 1.2
+    if tres is not None:                                             # :237-252
+        step = max(1, int(round(fs * tres / 1e6)))
+        step = max(1, min(step, nsig // 10))
+        ws = min(max(base, step * 2), nsig)
+        overlap = max(0, ws - step * 2) if heavy else max(0, ws - step)
+    else:                                                            # :253-259
+        ws = min(base, nsig)
+        overlap = int(ws * 0.75) if heavy else int(ws * 0.90)
+    nfft = max(256, int(2 ** np.ceil(np.log2(ws * frf))))           # :262
+    nfft = min(nfft, 1024) if heavy else max(nfft, 512)              # :265-268
+    window = "hann" if heavy else "blackmanharris"                   # :273-276
+    return dict(factor=factor, fs=fs, nsig=nsig, window=window, nperseg=ws,
+                noverlap=overlap, nfft=nfft, heavy=heavy)
+
+
+def _all_zero(S) -> bool:
+    """np.max(Sxx) == 0 (utils.py:316) — reduced on the GPU."""
+    if isinstance(S, torch.Tensor):
+        _, mx, _, _, _ = dsp.peak_stats(S.T.contiguous().view(-1))
+    else:
+        _, mx, _, _, _ = dsp.peak_stats(np.ascontiguousarray(S).ravel())
+    return mx == 0.0
+
+
+def create_spectrogram(sig, sr, center_freq=0, max_samples=2_000_000, time_resolution_us=1,
+                       adaptive_resolution=True):
+    """Drop-in for utils.create_spectrogram: returns (freqs, times, Sxx) with
+    Sxx (nfft, nframes), fftshift-ed along frequency, freqs shifted, scaled by
+    the decimation factor and offset by center_freq."""
+    dev = isinstance(sig, torch.Tensor)
+    n = int(sig.shape[0]) if dev else len(sig)
+    p = spectrogram_params(n, sr, max_samples, time_resolution_us, adaptive_resolution)
+    factor, fs = p["factor"], p["fs"]
+    if dev:
+        x = sig if sig.dtype == torch.complex64 else sig.to(torch.complex64)
+        x = x.contiguous()
+        kw = dict(_stride=factor, _nsamples=p["nsig"])
+    else:
+        x = np.asarray(sig)
+        if factor > 1:
+            x = x[::factor]                    # only the kept samples cross PCIe
+        kw = {}
+
+    def stft(window, nperseg, noverlap, nfft):
+        return dsp.spectrum(x, fs, window, nperseg, noverlap, nfft, fftshift=True, **kw)
+
+    try:                                                              # utils.py:279-313
+        freqs, times, Sxx = stft(p["window"], p["nperseg"], p["noverlap"], p["nfft"])
+    except ValueError:   # what scipy raises for these arguments (e.g. nfft < nperseg)
+        ws = min(256, p["nsig"])
+        freqs, times, Sxx = stft("hann", ws, ws // 2, 512)
+    if _all_zero(Sxx):                                                # utils.py:316-347
+        ws = min(64, p["nsig"] // 4)
+        try:
+            freqs, times, Sxx = stft("hann", ws, ws // 4, max(128, ws))
+        except ValueError:
+            freqs, times, Sxx = stft("boxcar", 32, 16, 64)
+    freqs = np.fft.fftshift(freqs) * factor + center_freq             # utils.py:350
+    return freqs, times, Sxx
