@@ -75,7 +75,8 @@ const char* vsig_errstr(int status);
 int vsig_init(int device, vsig_ctx** out);
 void vsig_free(vsig_ctx* ctx);
 const char* vsig_last_error(const vsig_ctx* ctx);
-/* hip_stream: a hipStream_t, or NULL for the context's own stream. */
+/* hip_stream: the hipStream_t to enqueue on; NULL is the default (null)
+ * stream.  A new context starts on a private non-blocking stream. */
 int vsig_set_stream(vsig_ctx* ctx, void* hip_stream);
 int vsig_synchronize(vsig_ctx* ctx);
 /* Per-kernel timing with HIP events on the context stream (for bench.py):

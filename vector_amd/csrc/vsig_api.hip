@@ -238,7 +238,7 @@ const char* vsig_last_error(const vsig_ctx* c) { return c ? c->err.c_str() : "nu
 
 int vsig_set_stream(vsig_ctx* c, void* s) {
   if (!c) return VSIG_E_INVALID;
-  c->stream = s ? (hipStream_t)s : c->own;
+  c->stream = (hipStream_t)s;  // NULL is the device's default (null) stream
   return VSIG_OK;
 }
 
