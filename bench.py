@@ -1,0 +1,233 @@
+"""Benchmark: Msamples/s of complex64 IQ through the FIR -> (decimate) -> FFT-PSD
+-> xcorr-sync chain on 1..N MI355X GPUs, with the dominant kernel's achieved
+HBM bandwidth against the roofline and the CPU reference path beside it.
+
+Workload (BASELINE.json configs[1], extended with the sync stage the metric
+names): every rank owns a contiguous 2**28-sample (256 Msample, 2 GiB) time
+chunk of one long synthetic capture; 255-tap overlap-save FIR, D = 1;
+8192-point Hann PSD, hop 8192; 4096-sample template valid correlation with a
+fused |c| argmax.  Weak scaling: N GPUs process an N x 256 Msample capture
+(N = 8 is BASELINE config 5's 2**31 samples), exchanging only the FIR /
+correlation halos and 32-byte peak records over RCCL.
+
+  python bench.py [--gpus N --steps K --warmup W]
+  python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Inputs are generated on the device before timing (data resident in HBM).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Msamples/s c64 through FIR+FFT+xcorr chain; 1/2/4/8 GPU + %HBM roofline"
+HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+TONES = ((1.0, 0.05), (0.5, 0.11), (0.25, -0.20))
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def design(ntaps, L):
+    import scipy.signal
+    taps = scipy.signal.firwin(ntaps, 0.2).astype(np.float32)
+    rng = np.random.default_rng(4096)
+    b = rng.integers(0, 2, size=(2, L))
+    pre = (((2 * b[0] - 1) + 1j * (2 * b[1] - 1)) / np.sqrt(2)).astype(np.complex64)
+    # The template is the preamble as it leaves the receive filter (causal part),
+    # so the filtered capture contains it exactly at the planted offset.
+    tmpl = np.convolve(pre, taps)[:L].astype(np.complex64)
+    return taps, pre, tmpl
+
+
+def generate_chunk(x: torch.Tensor, g0: int, seed: int, pre: np.ndarray, k0: int):
+    """x[i] = sum_t A_t exp(j 2 pi f_t (g0 + i)) + CN(0,1) noise (+ preamble at
+    global sample k0), written in place on the device, in 2**24-sample slabs."""
+    n = x.shape[0]
+    gen = torch.Generator(device=x.device)
+    gen.manual_seed(seed)
+    slab = 1 << 24
+    for s in range(0, n, slab):
+        m = min(slab, n - s)
+        idx = torch.arange(g0 + s, g0 + s + m, device=x.device, dtype=torch.float64)
+        acc = torch.randn(m, dtype=torch.complex64, device=x.device, generator=gen)
+        for a, f in TONES:
+            ph = torch.remainder(idx * f, 1.0) * (2 * np.pi)
+            acc += (a * torch.polar(torch.ones_like(ph), ph)).to(torch.complex64)
+        x[s:s + m] = acc
+    lo, hi = max(k0, g0), min(k0 + len(pre), g0 + n)
+    if lo < hi:
+        x[lo - g0:hi - g0] += torch.from_numpy(pre[lo - k0:hi - k0]).to(x.device)
+
+
+def cpu_baseline(samples, taps, nfft, tmpl):
+    """The reference's CPU path (oracle: np.convolve / scipy.signal.spectrogram /
+    np.correlate, single-threaded numpy) timed on a bounded sample."""
+    from oracle import ref
+    x = ref.synth_iq(samples, seed=99)
+    t0 = time.perf_counter()
+    y = ref.fir_filter(x, taps, 1)
+    ref.spectrum(y, 1.0, "hann", nfft, 0, nfft)
+    c, lags = ref.cross_correlate_signals(tmpl, y, "valid")
+    ref.find_correlation_peak(c, lags)
+    dt = time.perf_counter() - t0
+    return dict(value=round(samples / dt / 1e6, 3), unit="Msamples/s", cores=1, kind="port",
+                sample=(f"{samples} samples (2**{int(np.log2(samples))}) of the same chain: "
+                        f"np.convolve {len(taps)} taps, scipy spectrogram nfft={nfft}, "
+                        f"np.correlate complex128 L={len(tmpl)} valid + find_correlation_peak; "
+                        f"{dt:.2f} s, 1 thread"),
+                seconds=round(dt, 3))
+
+
+def load_traffic(key):
+    """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary
+    (profiles/pmc_*.json, corrected as MI355X_MICROARCH.md §HBM prescribes)."""
+    import glob
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("config_key") == key:
+            best = d
+    return best
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--samples", type=int, default=1 << 28, help="input samples per GPU")
+    ap.add_argument("--ntaps", type=int, default=255)
+    ap.add_argument("--decim", type=int, default=1)
+    ap.add_argument("--nfft", type=int, default=8192)
+    ap.add_argument("--template", type=int, default=4096)
+    ap.add_argument("--cpu-samples", type=int, default=1 << 22)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
+                         "python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+    torch.cuda.set_device(local)
+    dev = torch.device(f"cuda:{local}")
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import vector_amd  # noqa: F401
+    from vector_amd.shard import ChainConfig, HipBackend, StreamChain
+
+    n = args.samples
+    taps, pre, tmpl = design(args.ntaps, args.template)
+    cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl)
+    be = HipBackend(cfg, local)
+    chain = StreamChain(cfg, be, rank, world)
+    N = world * n
+    ny_total = N // args.decim
+    k0 = (ny_total // 2 + 12_345) * args.decim     # global input sample of the preamble
+    generate_chunk(chain.x, rank * n, 20250718 + rank, pre, k0)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        chain.step()
+    torch.cuda.synchronize()
+    barrier()
+    lib, h = be.ctx.lib, be.ctx.h
+    lib.vsig_timing_reset(h)
+    lib.vsig_timing_enable(h, 0 if args.no_kernel_timing else 1)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        chain.step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    lib.vsig_timing_enable(h, 0)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel durations from HIP events on the launch stream
+    import ctypes as C
+    stages = {}
+    for name in ("fir", "psd", "xcorr"):
+        tot, cnt = C.c_double(), C.c_int64()
+        lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
+        if cnt.value:
+            stages[name] = tot.value / cnt.value
+    ny = n // args.decim
+    bytes_per_launch = {"fir": 8 * n + 8 * ny, "psd": 8 * ny + 4 * ny,
+                        "xcorr": 8 * (ny + chain.yhalo)}
+    m, lag, s1, s2, nout = chain.global_peak()
+    check = {"sync_lag": lag, "expected": k0 // args.decim, "ok": bool(lag == k0 // args.decim)}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    ms_per_step = elapsed / args.steps * 1e3
+    value = N / (elapsed / args.steps) / 1e6
+    roof = None
+    if stages:
+        dom = max(stages, key=lambda k: stages[k])
+        achieved = bytes_per_launch[dom] / (stages[dom] * 1e-3) / 1e9
+        key = f"{dom}:n={n}:ntaps={args.ntaps}:decim={args.decim}:nfft={args.nfft}:L={args.template}"
+        pmc = load_traffic(key)
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "algorithmic_bytes": bytes_per_launch[dom],
+                "avg_launch_ms": round(stages[dom], 4),
+                "traffic_source": pmc["source"] if pmc else None}
+    cpu = None
+    if world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_samples, taps, args.nfft, tmpl)
+        cpu["cores_available"] = len(os.sched_getaffinity(0))
+    out = {
+        "metric": METRIC, "value": round(value, 1), "unit": "Msamples/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c64 (fp32)",
+        "data": "synthetic IQ generated on device: 3 tones + CN(0,1) noise + QPSK preamble",
+        "config": {"workload": (f"BASELINE configs[1] chain + sync: {n} c64 samples/GPU, "
+                                f"{args.ntaps}-tap overlap-save FIR, D={args.decim}, "
+                                f"{args.nfft}-pt Hann PSD hop {args.nfft}, "
+                                f"{args.template}-sample template xcorr (valid) + argmax"),
+                   "samples_per_gpu": n, "total_samples": N, "ntaps": args.ntaps,
+                   "decim": args.decim, "nfft": args.nfft, "template": args.template,
+                   "parallelism": f"time-chunk x{world} (RCCL halos)"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+        "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "check": check,
+    }
+    print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

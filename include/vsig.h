@@ -104,6 +104,12 @@ int vsig_psd_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* win, int3
 int vsig_fir_create(vsig_ctx* ctx, const void* taps, int32_t ntaps, int32_t decim, vsig_fir** out);
 void vsig_fir_free(vsig_fir* fir);
 int vsig_fir_exec_dev(vsig_fir* fir, const void* x, int64_t n, void* y, int64_t ny);
+/* Time-chunk form: x points at nhist history samples (the previous chunk's
+ * last samples, the left halo) followed by the n samples to filter; y gets the
+ * ceil(n/decim) outputs of those n samples, exactly as if the whole stream
+ * had been filtered at once. */
+int vsig_fir_exec_hist_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t n, void* y,
+                           int64_t ny);
 int vsig_fir_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* taps, int32_t ntaps,
                  int32_t decim, void* y, int64_t ny);
 

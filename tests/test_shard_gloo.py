@@ -1,0 +1,141 @@
+"""Multi-rank (world_size 2 and 3) CPU test of the time-chunk sharding with the
+gloo backend: halos, frame alignment and the global argmax must reproduce the
+single-stream result exactly.  Per-rank compute uses the CPU oracle as a
+stand-in backend (this test checks the orchestration, not the kernels)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import ref
+
+
+class OracleBackend:
+    """CPU stand-in with HipBackend's interface (test infrastructure)."""
+
+    def __init__(self, cfg):
+        self.cfg = cfg
+
+    def empty(self, n, dtype=torch.complex64):
+        return torch.zeros(n, dtype=dtype)
+
+    def fir_into(self, x_ext, nhist, y):
+        x = x_ext.numpy()
+        full = np.convolve(x, self.cfg.taps)[nhist: len(x)]
+        y.copy_(torch.from_numpy(full[:: self.cfg.decim].astype(np.complex64)))
+
+    def psd_into(self, y, sxx):
+        _, _, S = ref.spectrum(y.numpy(), 1.0, "hann", self.cfg.nfft, 0, self.cfg.nfft)
+        sxx.copy_(torch.from_numpy(np.ascontiguousarray(S.T).ravel()))
+
+    def xcorr_peak(self, s):
+        c = np.correlate(s.numpy().astype(np.complex128),
+                         self.cfg.template.astype(np.complex128), "valid")
+        a = np.abs(c)
+        i = int(np.argmax(a))
+        rec = torch.tensor([a[i], 0.0, a.sum(), (a * a).sum()], dtype=torch.float64)
+        rec.view(torch.int64)[1] = i
+        return rec
+
+
+def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
+    rng = np.random.default_rng(world)
+    N = world * n_local
+    x = ref.synth_iq(N, seed=world)
+    taps = rng.standard_normal(ntaps).astype(np.float32)
+    pre = ref.qpsk_preamble(L, seed=7)
+    k0 = k0 if k0 is not None else n_local // decim - L // 2     # straddles the first boundary
+    y_full = np.convolve(x, taps)[:N][::decim].astype(np.complex64)
+    y_full[k0:k0 + L] += 6 * pre                                   # plant after filtering
+    return x, taps, pre, k0, y_full
+
+
+def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vector_amd.shard import ChainConfig, StreamChain
+        x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L)
+        cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre)
+        be = OracleBackend(cfg)
+
+        class PlantingBackend(OracleBackend):
+            """Adds the preamble to the filtered stream at global k0 (as the
+            single-stream reference does) before the PSD / xcorr stages."""
+            def fir_into(self, x_ext, nhist, y):
+                super().fir_into(x_ext, nhist, y)
+                ny = y.shape[0]
+                lo, hi = rank * ny, (rank + 1) * ny
+                a, b = max(lo, k0), min(hi, k0 + L)
+                if a < b:
+                    y[a - lo:b - lo] += torch.from_numpy((6 * pre[a - k0:b - k0]).astype(np.complex64))
+
+        be = PlantingBackend(cfg)
+        ch = StreamChain(cfg, be, rank, world)
+        ch.x.copy_(torch.from_numpy(x[rank * n_local:(rank + 1) * n_local]))
+        ch.step()
+        q.put((rank, ch.y.numpy().copy(), ch.sxx.numpy().copy(), ch.global_peak()))
+    finally:
+        dist.destroy_process_group()
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_chain_matches_single_stream(world):
+    n_local, decim, nfft, ntaps, L = 4096, 2, 256, 31, 100
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_local, decim, nfft, ntaps, L, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, y, sxx, pk = q.get(timeout=120)
+        res[r] = (y, sxx, pk)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    x, taps, pre, k0, y_full = make_case(world, n_local, decim, nfft, ntaps, L)
+    ny = n_local // decim
+    y_cat = np.concatenate([res[r][0] for r in range(world)])
+    np.testing.assert_allclose(y_cat, y_full, rtol=0, atol=1e-5 * np.abs(y_full).max())
+    _, _, S = ref.spectrum(y_full, 1.0, "hann", nfft, 0, nfft)
+    s_cat = np.concatenate([res[r][1] for r in range(world)]).reshape(-1, nfft)
+    np.testing.assert_allclose(s_cat, S.T, rtol=1e-5, atol=1e-6 * S.max())
+    i, lag, peak, s1, s2, conf = ref.xcorr_peak(y_full, pre, "valid")
+    for r in range(world):
+        m, gi, a, b, nout = res[r][2]
+        assert gi == lag == k0                                   # exact, on every rank
+        assert nout == world * ny - L + 1
+        assert m == pytest.approx(peak, rel=1e-6)
+        assert a == pytest.approx(s1, rel=1e-6) and b == pytest.approx(s2, rel=1e-6)
+
+
+def test_combine_peaks_tie_lowest_index():
+    from vector_amd.shard import combine_peaks
+    rows = np.array([(5.0, 900, 1.0, 2.0), (5.0, 100, 1.0, 2.0), (4.0, 3, 1.0, 2.0)], dtype=object)
+    m, i, s1, s2 = combine_peaks(rows)
+    assert (m, i, s1, s2) == (5.0, 100, 3.0, 6.0)
+
+
+def test_chain_config_validation():
+    from vector_amd.shard import ChainConfig
+    with pytest.raises(ValueError):
+        ChainConfig(n_local=1000, taps=np.ones(3), decim=3, nfft=64).validate(2)
+    with pytest.raises(ValueError):
+        ChainConfig(n_local=1024, taps=np.ones(3), decim=1, nfft=1000).validate(2)
+    with pytest.raises(ValueError):
+        ChainConfig(n_local=128, taps=np.ones(3), nfft=64, template=np.ones(500)).validate(2)

@@ -52,6 +52,7 @@ SIGNATURES = {
     "vsig_fir_create": (C.c_int, [P, P, I32, I32, C.POINTER(P)]),
     "vsig_fir_free": (None, [P]),
     "vsig_fir_exec_dev": (C.c_int, [P, P, I64, P, I64]),
+    "vsig_fir_exec_hist_dev": (C.c_int, [P, P, I64, I64, P, I64]),
     "vsig_fir_c64": (C.c_int, [P, P, I64, P, I32, I32, P, I64]),
     "vsig_xcorr_create": (C.c_int, [P, P, I32, C.POINTER(P)]),
     "vsig_xcorr_free": (None, [P]),

@@ -106,15 +106,16 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
 
 // ---------------------------------------------------------------------------
 // FIR, overlap-save.  Block b produces outputs g in [b*hop, b*hop + hop) of
-//   y[g] = sum_{m < ntaps} h[m] x[g - m]   (x = 0 outside [0, n))
-// i.e. np.convolve(x, h, 'full')[:n]; only g % decim == 0 is stored, at g/decim.
+//   y[g] = sum_{m < ntaps} h[m] x[g0 + g - m]   (x = 0 outside [0, n))
+// i.e. np.convolve(x, h, 'full')[g0:n]; only g % decim == 0 is stored, at
+// g/decim.  The first g0 samples are history (a time-chunk's left halo).
 // The segment x[b*hop - (ntaps-1) .. + M) is FFT'd, multiplied by Hs = FFT(h)/M
 // and inverse-transformed (conj trick), all in LDS / registers.
 // ---------------------------------------------------------------------------
 template <class P>
 __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
-    const float2* __restrict__ x, long long n, const float2* __restrict__ Hs, int ntaps,
-    long long hop, int decim, float2* __restrict__ y, long long nblocks,
+    const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
+    int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
     const float2* __restrict__ tw) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   constexpr int BT = block_threads<P>();
@@ -123,7 +124,7 @@ __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
   const int t = threadIdx.x;
   const long long b = blockIdx.x;
   if (b >= nblocks) return;  // uniform per block
-  const long long s0 = b * hop - (ntaps - 1);
+  const long long s0 = g0 + b * hop - (ntaps - 1);
 
   float2 v[P::E];
   load_segment<P>(v, x, s0, n, t);
@@ -132,11 +133,12 @@ __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
   for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
   fft_frame<P>(v, lds, tw, t);
   const int lo = ntaps - 1;
+  const long long nloc = n - g0;
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = out_index<P>(t, e) - lo;
-    const long long g = b * hop + i;
-    if (i >= 0 && i < hop && g < n && (decim == 1 || g % decim == 0))
+    const long long g = b * hop + i;          // output index relative to g0
+    if (i >= 0 && i < hop && g < nloc && (decim == 1 || g % decim == 0))
       y[decim == 1 ? g : g / decim] = cconj(v[e]);
   }
 }
@@ -326,13 +328,14 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
     default: return hipErrorInvalidValue;                  \
   }
 
-hipError_t launch_fir_os(int M, const float2* x, long long n, const float2* Hs, int ntaps,
-                         long long hop, int decim, float2* y, const float2* tw, hipStream_t st) {
-  if (n <= 0) return hipSuccess;
-  const long long nblocks = (n + hop - 1) / hop;
+hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
+                         int ntaps, long long hop, int decim, float2* y, const float2* tw,
+                         hipStream_t st) {
+  if (n - g0 <= 0) return hipSuccess;
+  const long long nblocks = (n - g0 + hop - 1) / hop;
   VSIG_OS_SWITCH(M, {
     hipLaunchKernelGGL(fir_os_kernel<PL>, dim3((unsigned)nblocks), dim3(block_threads<PL>()), 0,
-                       st, x, n, Hs, ntaps, hop, decim, y, nblocks, tw);
+                       st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
   });
   return hipGetLastError();
 }

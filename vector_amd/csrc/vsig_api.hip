@@ -338,19 +338,24 @@ void vsig_fir_free(vsig_fir* f) {
   delete f;
 }
 
-int vsig_fir_exec_dev(vsig_fir* f, const void* x, int64_t n, void* y, int64_t ny) {
+int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y,
+                           int64_t ny) {
   if (!f) return VSIG_E_INVALID;
   vsig_ctx* c = f->ctx;
   if (!x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
-  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
   int rc = get_twiddles(c, f->M, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
-  HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, n, f->Hs, f->ntaps, f->hop, f->decim,
-                                (float2*)y, tw, c->stream));
+  HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,
+                                f->decim, (float2*)y, tw, c->stream));
   return VSIG_OK;
+}
+
+int vsig_fir_exec_dev(vsig_fir* f, const void* x, int64_t n, void* y, int64_t ny) {
+  return vsig_fir_exec_hist_dev(f, x, 0, n, y, ny);
 }
 
 int vsig_fir_c64(vsig_ctx* c, const void* x, int64_t n, const float* taps, int32_t ntaps,

@@ -21,8 +21,9 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                       const float2* tw, hipStream_t st);
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
                                 const float2* tw, hipStream_t st);
-hipError_t launch_fir_os(int M, const float2* x, long long n, const float2* Hs, int ntaps,
-                         long long hop, int decim, float2* y, const float2* tw, hipStream_t st);
+hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
+                         int ntaps, long long hop, int decim, float2* y, const float2* tw,
+                         hipStream_t st);
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, hipStream_t st);

@@ -205,14 +205,18 @@ class FirFilter:
     def out_len(self, n: int) -> int:
         return (n + self.decim - 1) // self.decim
 
-    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None) -> torch.Tensor:
-        """x: 1-D complex64 CUDA tensor -> complex64 CUDA tensor (async)."""
+    def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None,
+                 nhist: int = 0) -> torch.Tensor:
+        """x: 1-D complex64 CUDA tensor -> complex64 CUDA tensor (async).
+        The first nhist samples of x are history (a left halo): only the
+        remaining samples produce outputs."""
         self.ctx.bind_stream()
-        n = int(x.shape[0])
+        n = int(x.shape[0]) - int(nhist)
         ny = self.out_len(n)
         if out is None:
             out = torch.empty(ny, dtype=torch.complex64, device=x.device)
-        self.ctx.check(self.ctx.lib.vsig_fir_exec_dev(self.h, _ptr(x), n, _ptr(out), ny), "filter")
+        self.ctx.check(self.ctx.lib.vsig_fir_exec_hist_dev(self.h, _ptr(x), int(nhist), n,
+                                                           _ptr(out), ny), "filter")
         return out
 
     def __del__(self):
