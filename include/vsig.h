@@ -79,6 +79,12 @@ const char* vsig_last_error(const vsig_ctx* ctx);
  * stream.  A new context starts on a private non-blocking stream. */
 int vsig_set_stream(vsig_ctx* ctx, void* hip_stream);
 int vsig_synchronize(vsig_ctx* ctx);
+/* Tuning knobs (defaults are the measured best on MI355X):
+ *   "psd_variant" / "fir_variant" / "xcorr_variant": bit 0 persistent kernel
+ *   (next-unit prefetch, register twiddles), bit 1 (M = 16384) 512-thread plan;
+ *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule.
+ * Plans created afterwards use the new block sizes. */
+int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 /* Per-kernel timing with HIP events on the context stream (for bench.py):
  * enable, run, then read the mean duration in ms of each kernel family. */
 int vsig_timing_enable(vsig_ctx* ctx, int on);

@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace vsig {
 
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
@@ -142,20 +144,72 @@ __device__ __forceinline__ void static_for(F&& f) {
   if constexpr (B < E) { f(IC<B>{}); static_for<B + 1, E>(f); }
 }
 
+// Twiddle sources for passes p >= 1.
+//  TwTable  : the global per-plan table (one load per element and pass).
+//  TwAnchors: per-thread register anchors w^a, a in {1, 8, 16, 24} (< R), read
+//             once per persistent block from the table; w^r is rebuilt per
+//             frame as anchor * w^(r mod 8) (a chain of at most 7 multiplies,
+//             |error| <~ 10 ulp).  Keeps every global load out of the FFT, so a
+//             prefetch of the next unit stays in flight across it (vmcnt is
+//             retired in issue order).
+struct TwTable { const float2* tw; };
+struct TwAnchors { const float2* wa; };
+
+template <class P>
+constexpr int nanch(int p) { return 1 + (P::R[p] - 1) / 8; }
+template <class P>
+constexpr int anch_off(int p) {
+  int o = 0;
+  for (int q = 1; q < p; ++q) o += (P::E / P::R[q]) * nanch<P>(q);
+  return o;
+}
+template <class P>
+constexpr int nanch_total() { return anch_off<P>(P::NP) > 0 ? anch_off<P>(P::NP) : 1; }
+
+// Load this thread's anchors (thread t of its frame).
+template <class P>
+__device__ __forceinline__ void load_anchors(float2* wa, const float2* __restrict__ tw, int t) {
+  static_for<1, P::NP>([&](auto pi) {
+    constexpr int p = decltype(pi)::value;
+    constexpr int R = P::R[p], Ns = P::ns(p), B = P::E / R, NA = nanch<P>(p);
+    static_for<0, B>([&](auto bi) {
+      constexpr int b = decltype(bi)::value;
+      const int k = (t + b * P::TF) & (Ns - 1);
+      static_for<0, NA>([&](auto ai) {
+        constexpr int a = decltype(ai)::value;
+        constexpr int r = a == 0 ? 1 : 8 * a;
+        wa[anch_off<P>(p) + b * NA + a] = tw[P::twoff(p) + (r - 1) * Ns + k];
+      });
+    });
+  });
+}
+
 // stage p: twiddle (p > 0) + register DFT for each of this thread's butterflies
-template <class P, int p>
-__device__ __forceinline__ void fft_stage(float2* v, const float2* __restrict__ tw, int t) {
+template <class P, int p, class TW>
+__device__ __forceinline__ void fft_stage(float2* v, TW tws, int t) {
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
   constexpr int B = P::E / R;
 #pragma unroll
   for (int b = 0; b < B; ++b) {
     if constexpr (p > 0) {
-      const int j = t + b * P::TF;
-      const int k = j & (Ns - 1);
-      const float2* twp = tw + P::twoff(p) + k;
+      if constexpr (std::is_same<TW, TwTable>::value) {
+        const int j = t + b * P::TF;
+        const int k = j & (Ns - 1);
+        const float2* twp = tws.tw + P::twoff(p) + k;
 #pragma unroll
-      for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], twp[(r - 1) * Ns]);
+        for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], twp[(r - 1) * Ns]);
+      } else {
+        constexpr int NA = nanch<P>(p);
+        const float2* wa = tws.wa + anch_off<P>(p) + b * NA;
+        const float2 w1 = wa[0];
+        float2 cur = w1;
+#pragma unroll
+        for (int r = 1; r < R; ++r) {
+          if (r > 1) cur = (r % 8 == 0) ? wa[r / 8] : cmul(cur, w1);
+          v[b * R + r] = cmul(v[b * R + r], cur);
+        }
+      }
     }
     dft_reg<R>(v + b * R);
   }
@@ -201,15 +255,15 @@ __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   });
 }
 
-template <class P, int p>
-__device__ __forceinline__ void fft_tail(float2* v, float2* lds, const float2* __restrict__ tw, int t) {
+template <class P, int p, class TW>
+__device__ __forceinline__ void fft_tail(float2* v, float2* lds, TW tws, int t) {
   if constexpr (p < P::NP) {
     __syncthreads();               // previous readers of lds are done
     fft_store<P, p - 1>(v, lds, t);
     __syncthreads();
     fft_load<P, p>(v, lds, t);
-    fft_stage<P, p>(v, tw, t);
-    fft_tail<P, p + 1>(v, lds, tw, t);
+    fft_stage<P, p>(v, tws, t);
+    fft_tail<P, p + 1>(v, lds, tws, t);
   }
 }
 
@@ -223,8 +277,26 @@ __device__ __forceinline__ void fft_frame(float2* v, float2* lds, const float2* 
   // otherwise have its twiddle loads CSE'd across them and keep every twiddle
   // of the first FFT live in VGPRs until the second.
   asm volatile("" : "+s"(tw));
-  fft_stage<P, 0>(v, tw, t);
-  fft_tail<P, 1>(v, lds, tw, t);
+  fft_stage<P, 0>(v, TwTable{tw}, t);
+  fft_tail<P, 1>(v, lds, TwTable{tw}, t);
+}
+
+// Opaque to the optimiser: stops LICM from hoisting the per-frame twiddle
+// powers (loop-invariant functions of the anchors) out of a persistent loop,
+// which would pin every twiddle of the plan in VGPRs.
+template <class P>
+__device__ __forceinline__ void launder_anchors(float2* wa) {
+#pragma unroll
+  for (int i = 0; i < nanch_total<P>(); ++i) asm volatile("" : "+v"(wa[i].x), "+v"(wa[i].y));
+}
+
+// The same with register-resident twiddle anchors (see TwAnchors).
+template <class P>
+__device__ __forceinline__ void fft_frame_anch(float2* v, float2* lds, float2* wa, int t) {
+  static_assert(P::valid(), "invalid FFT plan");
+  launder_anchors<P>(wa);
+  fft_stage<P, 0>(v, TwAnchors{wa}, t);
+  fft_tail<P, 1>(v, lds, TwAnchors{wa}, t);
 }
 
 // Index helpers for the operand / result layout.

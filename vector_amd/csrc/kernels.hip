@@ -15,11 +15,30 @@
 namespace vsig {
 
 // ---------------------------------------------------------------------------
-// spectrum: one frame per TF threads, frames = (n - nperseg) / hop + 1
+// Persistent-kernel skeleton shared by the streaming kernels: a block walks
+// units u = blockIdx.x, + gridDim.x, ...; the next unit's samples are loaded
+// into registers at the top of each iteration, so their HBM latency hides
+// behind the current unit's FFTs (the only global loads in flight are stream
+// loads: twiddles, window and filter spectra live in registers).
+// ---------------------------------------------------------------------------
+
+// spectrum: frames = (n - nperseg) / hop + 1; FPB frames per unit
 // (scipy.signal.spectrogram, scipy/signal/_spectral_py.py:2158-2205, as called
 // at utils.py:281-291).
-// ---------------------------------------------------------------------------
 template <class P>
+__device__ __forceinline__ void psd_load(float2* v, const float2* __restrict__ x, long long stride,
+                                         int nperseg, long long hop, long long frame,
+                                         long long nframes, int t) {
+  const bool active = frame < nframes;
+  const float2* xf = x + (active ? frame * hop * stride : 0);
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const int i = in_index<P>(t, e);
+    v[e] = (active && i < nperseg) ? xf[(long long)i * stride] : make_float2(0.f, 0.f);
+  }
+}
+
+template <class P, int PERSIST>
 __global__ __launch_bounds__(block_threads<P>()) void psd_kernel(
     const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
@@ -29,30 +48,61 @@ __global__ __launch_bounds__(block_threads<P>()) void psd_kernel(
   __shared__ float2 lds[FPB * P::LDS];
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
-  const long long frame = (long long)blockIdx.x * FPB + fl;
-  const bool active = frame < nframes;
-  const float2* xf = x + (active ? frame * hop * stride : 0);
+  const long long units = (nframes + FPB - 1) / FPB;
+  long long u = blockIdx.x;
+  if (u >= units) return;
 
-  float2 v[P::E];
+  if constexpr (!PERSIST) {          // one unit per block, table twiddles
+    float2 v[P::E];
+    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = in_index<P>(t, e);
+      const float w = i < nperseg ? win[i] : 0.f;
+      v[e] = make_float2(v[e].x * w, v[e].y * w);
+    }
+    fft_frame<P>(v, lds + fl * P::LDS, tw, t);
+    const long long frame = u * FPB + fl;
+    if (frame < nframes) {
+      float* of = out + frame * P::N;
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = out_index<P>(t, e);
+        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+      }
+    }
+    return;
+  }
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float wr[P::E];
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = in_index<P>(t, e);
-    float2 a = make_float2(0.f, 0.f);
-    if (active && i < nperseg) {
-      const float2 s = xf[(long long)i * stride];
-      const float w = win[i];
-      a = make_float2(s.x * w, s.y * w);
-    }
-    v[e] = a;
+    wr[e] = i < nperseg ? win[i] : 0.f;
   }
-  fft_frame<P>(v, lds + fl * P::LDS, tw, t);
-  if (!active) return;
-  float* of = out + frame * P::N;
+  float2 v[P::E];
+  psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
+  for (; u < units; u += gridDim.x) {
+    float2 nv[P::E];
+    const long long nu = u + gridDim.x;
+    if (nu < units) psd_load<P>(nv, x, stride, nperseg, hop, nu * FPB + fl, nframes, t);
 #pragma unroll
-  for (int e = 0; e < P::E; ++e) {
-    const int i = out_index<P>(t, e);
-    const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-    of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+    for (int e = 0; e < P::E; ++e) v[e] = make_float2(v[e].x * wr[e], v[e].y * wr[e]);
+    fft_frame_anch<P>(v, lds + fl * P::LDS, wa, t);
+    const long long frame = u * FPB + fl;
+    if (frame < nframes) {
+      float* of = out + frame * P::N;
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = out_index<P>(t, e);
+        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = nv[e];
   }
 }
 
@@ -112,7 +162,7 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
 // The segment x[b*hop - (ntaps-1) .. + M) is FFT'd, multiplied by Hs = FFT(h)/M
 // and inverse-transformed (conj trick), all in LDS / registers.
 // ---------------------------------------------------------------------------
-template <class P>
+template <class P, int PERSIST>
 __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
@@ -122,24 +172,50 @@ __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
   static_assert(BT == P::TF, "one frame per block");
   __shared__ float2 lds[P::LDS];
   const int t = threadIdx.x;
-  const long long b = blockIdx.x;
+  long long b = blockIdx.x;
   if (b >= nblocks) return;  // uniform per block
-  const long long s0 = g0 + b * hop - (ntaps - 1);
 
-  float2 v[P::E];
-  load_segment<P>(v, x, s0, n, t);
-  fft_frame<P>(v, lds, tw, t);
-#pragma unroll
-  for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-  fft_frame<P>(v, lds, tw, t);
   const int lo = ntaps - 1;
   const long long nloc = n - g0;
+  if constexpr (!PERSIST) {          // one unit per block, table twiddles
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame<P>(v, lds, tw, t);
 #pragma unroll
-  for (int e = 0; e < P::E; ++e) {
-    const int i = out_index<P>(t, e) - lo;
-    const long long g = b * hop + i;          // output index relative to g0
-    if (i >= 0 && i < hop && g < nloc && (decim == 1 || g % decim == 0))
-      y[decim == 1 ? g : g / decim] = cconj(v[e]);
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e) - lo;
+      const long long g = b * hop + i;
+      if (i >= 0 && i < hop && g < nloc && (decim == 1 || g % decim == 0))
+        y[decim == 1 ? g : g / decim] = cconj(v[e]);
+    }
+    return;
+  }
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 v[P::E];
+  load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+  for (; b < nblocks; b += gridDim.x) {
+    fft_frame_anch<P>(v, lds, wa, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    // Prefetch after the (L2-resident) filter-spectrum loads: vmcnt retires in
+    // issue order, so the next segment then lands behind the inverse FFT.
+    float2 nv[P::E];
+    const long long nb = b + gridDim.x;
+    if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
+    fft_frame_anch<P>(v, lds, wa, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e) - lo;
+      const long long g = b * hop + i;          // output index relative to g0
+      if (i >= 0 && i < hop && g < nloc && (decim == 1 || g % decim == 0))
+        y[decim == 1 ? g : g / decim] = cconj(v[e]);
+    }
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = nv[e];
   }
 }
 
@@ -185,27 +261,12 @@ __device__ __forceinline__ void block_partial(double m, long long mi, double s1,
 // Epilogue: optional store of c (or of conj(c) at nout-1-o, for the swapped
 // argument order of np.correlate), and the block's |c| partial.
 // ---------------------------------------------------------------------------
+// Epilogue of one correlation block: |c|^2, block argmax / sums, optional store.
 template <class P>
-__global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
-    const float2* __restrict__ s, long long n, const float2* __restrict__ Ps, long long off,
-    long long nout, long long hop, float2* __restrict__ c, int store_mode,
-    PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw) {
-  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+__device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, long long hop,
+                                               long long nout, float2* __restrict__ c,
+                                               int store_mode, PeakPartial* partials, int t) {
   constexpr int BT = block_threads<P>();
-  static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[P::LDS];
-  const int t = threadIdx.x;
-  const long long b = blockIdx.x;
-  if (b >= nblocks) return;
-  const long long s0 = b * hop - off;
-
-  float2 v[P::E];
-  load_segment<P>(v, s, s0, n, t);
-  fft_frame<P>(v, lds, tw, t);
-#pragma unroll
-  for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
-  fft_frame<P>(v, lds, tw, t);
-
   float m = -1.f;
   long long mi = 0x7fffffffffffffffLL;
   float s1 = 0.f, s2 = 0.f;
@@ -224,6 +285,47 @@ __global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
     }
   }
   if (partials) block_partial<BT>((double)m, mi, (double)s1, (double)s2, partials + b);
+}
+
+template <class P, int PERSIST>
+__global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
+    const float2* __restrict__ s, long long n, const float2* __restrict__ Ps, long long off,
+    long long nout, long long hop, float2* __restrict__ c, int store_mode,
+    PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw) {
+  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+  constexpr int BT = block_threads<P>();
+  static_assert(BT == P::TF, "one frame per block");
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  long long b = blockIdx.x;
+  if (b >= nblocks) return;
+
+  if constexpr (!PERSIST) {          // one unit per block, table twiddles
+    float2 v[P::E];
+    load_segment<P>(v, s, b * hop - off, n, t);
+    fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+    fft_frame<P>(v, lds, tw, t);
+    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+    return;
+  }
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 v[P::E];
+  load_segment<P>(v, s, b * hop - off, n, t);
+  for (; b < nblocks; b += gridDim.x) {
+    fft_frame_anch<P>(v, lds, wa, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+    float2 nv[P::E];   // prefetch behind the template-spectrum loads (see fir_os_kernel)
+    const long long nb = b + gridDim.x;
+    if (nb < nblocks) load_segment<P>(nv, s, nb * hop - off, n, t);
+    fft_frame_anch<P>(v, lds, wa, t);
+    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = nv[e];
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -282,30 +384,56 @@ __global__ __launch_bounds__(1024) void partial_finalize(const PeakPartial* __re
 // ---------------------------------------------------------------------------
 // Host-side launchers (called from vsig_api.hip), dispatching N to plans.
 // ---------------------------------------------------------------------------
-#define VSIG_PLAN_SWITCH(N, BODY)                          \
+// Resident blocks of a persistent kernel: CUs x blocks per CU (occupancy API).
+template <class K>
+long long persistent_grid(K kernel, int block, long long units) {
+  static thread_local int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || per < 1)
+    per = 1;
+  const long long g = (long long)cus * per;
+  return units < g ? units : g;
+}
+
+#define VSIG_PLAN_SWITCH(N, ...)                          \
   switch (N) {                                             \
-    case 64: { using PL = Plan64; BODY; } break;           \
-    case 128: { using PL = Plan128; BODY; } break;         \
-    case 256: { using PL = Plan256; BODY; } break;         \
-    case 512: { using PL = Plan512; BODY; } break;         \
-    case 1024: { using PL = Plan1024; BODY; } break;       \
-    case 2048: { using PL = Plan2048; BODY; } break;       \
-    case 4096: { using PL = Plan4096; BODY; } break;       \
-    case 8192: { using PL = Plan8192; BODY; } break;       \
-    case 16384: { using PL = Plan16384; BODY; } break;     \
+    case 64: { using PL = Plan64; __VA_ARGS__; } break;           \
+    case 128: { using PL = Plan128; __VA_ARGS__; } break;         \
+    case 256: { using PL = Plan256; __VA_ARGS__; } break;         \
+    case 512: { using PL = Plan512; __VA_ARGS__; } break;         \
+    case 1024: { using PL = Plan1024; __VA_ARGS__; } break;       \
+    case 2048: { using PL = Plan2048; __VA_ARGS__; } break;       \
+    case 4096: { using PL = Plan4096; __VA_ARGS__; } break;       \
+    case 8192: { using PL = Plan8192; __VA_ARGS__; } break;       \
+    case 16384: { using PL = Plan16384; __VA_ARGS__; } break;     \
     default: return hipErrorInvalidValue;                  \
   }
 
+template <class PL, int PERSIST>
+void launch_psd_t(const float2* x, long long stride, const float* win, int nperseg, long long hop,
+                  float scale, float* out, long long nframes, int shift, const float2* tw,
+                  hipStream_t st) {
+  constexpr int BT = block_threads<PL>();
+  constexpr int FPB = BT / PL::TF;
+  const long long units = (nframes + FPB - 1) / FPB;
+  const long long grid = PERSIST ? persistent_grid(psd_kernel<PL, 1>, BT, units) : units;
+  hipLaunchKernelGGL((psd_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(BT), 0, st, x, stride,
+                     win, nperseg, hop, scale, out, nframes, shift, tw);
+}
+
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
                       long long hop, float scale, float* out, long long nframes, int shift,
-                      const float2* tw, hipStream_t st) {
+                      const float2* tw, int variant, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
   VSIG_PLAN_SWITCH(N, {
-    constexpr int BT = block_threads<PL>();
-    constexpr int FPB = BT / PL::TF;
-    const long long grid = (nframes + FPB - 1) / FPB;
-    hipLaunchKernelGGL(psd_kernel<PL>, dim3((unsigned)grid), dim3(BT), 0, st, x, stride, win,
-                       nperseg, hop, scale, out, nframes, shift, tw);
+    if (variant & 1) launch_psd_t<PL, 1>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    else launch_psd_t<PL, 0>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
   });
   return hipGetLastError();
 }
@@ -320,34 +448,61 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 }
 
 // Only plans with one frame per block can run the overlap-save kernels.
-#define VSIG_OS_SWITCH(N, BODY)                            \
-  switch (N) {                                             \
-    case 4096: { using PL = Plan4096; BODY; } break;       \
-    case 8192: { using PL = Plan8192; BODY; } break;       \
-    case 16384: { using PL = Plan16384; BODY; } break;     \
-    default: return hipErrorInvalidValue;                  \
+// variant bit 0: persistent (prefetch + register anchors); bit 1: the E = 32 /
+// 512-thread plan for M = 16384 instead of E = 16 / 1024 threads.
+using Plan16384w = Plan<16384, 32, 32, 16, 32>;
+#define VSIG_OS_SWITCH(N, V, ...)                                          \
+  switch (N) {                                                              \
+    case 4096: { using PL = Plan4096; __VA_ARGS__; } break;                        \
+    case 8192: { using PL = Plan8192; __VA_ARGS__; } break;                        \
+    case 16384:                                                             \
+      if ((V) & 2) { using PL = Plan16384w; __VA_ARGS__; }                         \
+      else { using PL = Plan16384; __VA_ARGS__; }                                  \
+      break;                                                                \
+    default: return hipErrorInvalidValue;                                   \
   }
+
+template <class PL, int PERSIST>
+void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, int ntaps,
+                  long long hop, int decim, float2* y, long long nblocks, const float2* tw,
+                  hipStream_t st) {
+  const long long grid =
+      PERSIST ? persistent_grid(fir_os_kernel<PL, 1>, block_threads<PL>(), nblocks) : nblocks;
+  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(block_threads<PL>()),
+                     0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
+}
 
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
-                         hipStream_t st) {
+                         int variant, hipStream_t st) {
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
-  VSIG_OS_SWITCH(M, {
-    hipLaunchKernelGGL(fir_os_kernel<PL>, dim3((unsigned)nblocks), dim3(block_threads<PL>()), 0,
-                       st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
+  VSIG_OS_SWITCH(M, variant, {
+    if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else launch_fir_t<PL, 0>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
   });
   return hipGetLastError();
 }
 
+template <class PL, int PERSIST>
+void launch_xcorr_t(const float2* s, long long n, const float2* Ps, long long off, long long nout,
+                    long long hop, float2* c, int store_mode, PeakPartial* partials,
+                    long long nblocks, const float2* tw, hipStream_t st) {
+  const long long grid =
+      PERSIST ? persistent_grid(xcorr_os_kernel<PL, 1>, block_threads<PL>(), nblocks) : nblocks;
+  hipLaunchKernelGGL((xcorr_os_kernel<PL, PERSIST>), dim3((unsigned)grid),
+                     dim3(block_threads<PL>()), 0, st, s, n, Ps, off, nout, hop, c, store_mode,
+                     partials, nblocks, tw);
+}
+
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
-                           PeakPartial* partials, const float2* tw, hipStream_t st) {
+                           PeakPartial* partials, const float2* tw, int variant, hipStream_t st) {
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
-  VSIG_OS_SWITCH(M, {
-    hipLaunchKernelGGL(xcorr_os_kernel<PL>, dim3((unsigned)nblocks), dim3(block_threads<PL>()),
-                       0, st, s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw);
+  VSIG_OS_SWITCH(M, variant, {
+    if (variant & 1) launch_xcorr_t<PL, 1>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+    else launch_xcorr_t<PL, 0>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
   });
   return hipGetLastError();
 }
@@ -374,6 +529,11 @@ hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, i
 
 namespace vsig {
 hipError_t plan_info(int N, int* radices, int* npasses) {
+  if (N == -16384) {   // the E = 32 plan of 16384 points (variant bit 1)
+    *npasses = Plan16384w::NP;
+    for (int q = 0; q < Plan16384w::NP; ++q) radices[q] = Plan16384w::R[q];
+    return hipSuccess;
+  }
   VSIG_PLAN_SWITCH(N, {
     *npasses = PL::NP;
     for (int q = 0; q < PL::NP; ++q) radices[q] = PL::R[q];

@@ -2,6 +2,7 @@
 // (twiddle tables, filter / template spectra), launch geometry, host staging.
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -29,6 +30,8 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
+  vsig::Variants var{1, 0, 0};           // tuned defaults (see vsig_set_option)
+  int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
 };
 
 struct vsig_fir {
@@ -67,6 +70,7 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
   int R[16], np = 0;
   if (vsig::plan_info(N, R, &np) != hipSuccess)
     return fail(c, VSIG_E_UNSUPPORTED, "FFT size " + std::to_string(N) + " not supported");
+  // (N < 0 keys an alternative plan of |N| points)
   std::vector<float2> h;
   int Ns = R[0];
   for (int p = 1; p < np; ++p) {
@@ -85,6 +89,8 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
   *out = d;
   return VSIG_OK;
 }
+
+int tw_key(int M, int variant) { return (M == 16384 && (variant & 2)) ? -16384 : M; }
 
 int ensure_partials(vsig_ctx* c, long long n) {
   if (n <= c->npartials) return VSIG_OK;
@@ -128,17 +134,36 @@ bool pow2_in(long long v, long long lo, long long hi) {
   return v >= lo && v <= hi && (v & (v - 1)) == 0;
 }
 
-int os_size_fir(int ntaps) {
+// VSIG_FIR_M / VSIG_XCORR_M: tuning overrides of the overlap-save block size.
+int env_size(const char* name, int dflt, int minlen) {
+  const char* e = getenv(name);
+  if (!e) return dflt;
+  const int v = atoi(e);
+  if ((v == 4096 || v == 8192 || v == 16384) && v >= 2 * minlen) return v;
+  return dflt;
+}
+
+int os_size_fir_default(int ntaps) {
   if (ntaps <= 512) return 4096;
   if (ntaps <= 2048) return 8192;
   if (ntaps <= 8192) return 16384;
   return 0;
 }
-int os_size_xcorr(int L) {
+int os_size_fir(const vsig_ctx* c, int ntaps) {
+  int d = os_size_fir_default(ntaps);
+  if (d && c->fir_m >= 2 * ntaps) d = c->fir_m;
+  return d ? env_size("VSIG_FIR_M", d, ntaps) : 0;
+}
+int os_size_xcorr_default(int L) {
   if (L <= 1024) return 4096;
   if (L <= 2048) return 8192;
   if (L <= 8192) return 16384;
   return 0;
+}
+int os_size_xcorr(const vsig_ctx* c, int L) {
+  int d = os_size_xcorr_default(L);
+  if (d && c->xcorr_m >= 2 * L) d = c->xcorr_m;
+  return d ? env_size("VSIG_XCORR_M", d, L) : 0;
 }
 
 // FFT_M(zero-padded u[0..len)) * gain into a new device buffer.
@@ -169,12 +194,12 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, int L, const float2* s, long
   int rc = ensure_partials(c, nblocks);
   if (rc) return rc;
   const float2* tw;
-  rc = get_twiddles(c, M, &tw);
+  rc = get_twiddles(c, tw_key(M, c->var.xcorr), &tw);
   if (rc) return rc;
   {
     Timed t(c, "xcorr");
     HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
-                                    c->partials, tw, c->stream));
+                                    c->partials, tw, c->var.xcorr, c->stream));
   }
   return finalize_peak(c, nblocks, 1, peak_dev);
 }
@@ -208,6 +233,9 @@ int vsig_init(int device, vsig_ctx** out) {
   c->device = device;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return VSIG_E_HIP; }
   c->stream = c->own;
+  if (const char* e = getenv("VSIG_PSD_VARIANT")) c->var.psd = atoi(e);
+  if (const char* e = getenv("VSIG_FIR_VARIANT")) c->var.fir = atoi(e);
+  if (const char* e = getenv("VSIG_XCORR_VARIANT")) c->var.xcorr = atoi(e);
   if (hipMalloc(&c->result, sizeof(PeakPartial)) != hipSuccess) { vsig_free(c); return VSIG_E_NOMEM; }
   *out = c;
   return VSIG_OK;
@@ -239,6 +267,22 @@ const char* vsig_last_error(const vsig_ctx* c) { return c ? c->err.c_str() : "nu
 int vsig_set_stream(vsig_ctx* c, void* s) {
   if (!c) return VSIG_E_INVALID;
   c->stream = (hipStream_t)s;  // NULL is the device's default (null) stream
+  return VSIG_OK;
+}
+
+int vsig_set_option(vsig_ctx* c, const char* key, int value) {
+  if (!c || !key) return VSIG_E_INVALID;
+  const std::string k(key);
+  if (k == "psd_variant") c->var.psd = value & 1;
+  else if (k == "fir_variant") c->var.fir = value & 3;
+  else if (k == "xcorr_variant") c->var.xcorr = value & 3;
+  else if (k == "fir_m" || k == "xcorr_m") {
+    if (value != 0 && value != 4096 && value != 8192 && value != 16384)
+      return fail(c, VSIG_E_INVALID, "block size must be 0, 4096, 8192 or 16384");
+    (k == "fir_m" ? c->fir_m : c->xcorr_m) = value;
+  } else {
+    return fail(c, VSIG_E_INVALID, "unknown option " + k);
+  }
   return VSIG_OK;
 }
 
@@ -286,7 +330,7 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
   if (rc) return rc;
   Timed t(c, "psd");
   HIPCHK(c, vsig::launch_psd(nfft, (const float2*)x, stride, win, nperseg, hop, scale, sxx, nframes,
-                             shift, tw, c->stream));
+                             shift, tw, c->var.psd, c->stream));
   return VSIG_OK;
 }
 
@@ -314,7 +358,7 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
   if (!c || !taps || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   *out = nullptr;
   if (ntaps < 1 || decim < 1) return fail(c, VSIG_E_INVALID, "ntaps and decim must be >= 1");
-  const int M = os_size_fir(ntaps);
+  const int M = os_size_fir(c, ntaps);
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "ntaps > 8192");
   long long hop = ((long long)M - (ntaps - 1)) / decim * decim;
   if (hop < 1) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
@@ -346,11 +390,11 @@ int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n,
   if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
-  int rc = get_twiddles(c, f->M, &tw);
+  int rc = get_twiddles(c, tw_key(f->M, c->var.fir), &tw);
   if (rc) return rc;
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,
-                                f->decim, (float2*)y, tw, c->stream));
+                                f->decim, (float2*)y, tw, c->var.fir, c->stream));
   return VSIG_OK;
 }
 
@@ -386,7 +430,7 @@ int vsig_xcorr_create(vsig_ctx* c, const void* tmpl, int32_t L, vsig_xcorr** out
   if (!c || !tmpl || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   *out = nullptr;
   if (L < 1) return fail(c, VSIG_E_INVALID, "template length must be >= 1");
-  const int M = os_size_xcorr(L);
+  const int M = os_size_xcorr(c, L);
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "template longer than 8192");
   float2* td = nullptr;
   HIPCHK(c, hipMalloc(&td, (size_t)L * sizeof(float2)));
@@ -436,7 +480,7 @@ int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v
   const float2* tmpl = (const float2*)(swap ? a : v);
   const float2* strm = (const float2*)(swap ? v : a);
   const int L = (int)nmin;
-  const int M = os_size_xcorr(L);
+  const int M = os_size_xcorr(c, L);
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "shorter operand longer than 8192");
   float2* Ps = nullptr;
   int rc = make_spectrum(c, tmpl, L, M, &Ps);

@@ -14,19 +14,24 @@ struct PeakPartial {
   double sum_abs2;   // sum |c|^2
 };
 
+// Radices of the plan for N points (N = -16384: the E = 32 plan of 16384).
 hipError_t plan_info(int N, int* radices, int* npasses);
+
+// Kernel variants (tuning): bit 0 persistent; bit 1 (M = 16384) E = 32 plan.
+struct Variants { int psd, fir, xcorr; };
 
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
                       long long hop, float scale, float* out, long long nframes, int shift,
-                      const float2* tw, hipStream_t st);
+                      const float2* tw, int variant, hipStream_t st);
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
                                 const float2* tw, hipStream_t st);
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
-                         hipStream_t st);
+                         int variant, hipStream_t st);
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
-                           PeakPartial* partials, const float2* tw, hipStream_t st);
+                           PeakPartial* partials, const float2* tw, int variant,
+                           hipStream_t st);
 hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
                               int nparts, hipStream_t st);
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
