@@ -118,6 +118,10 @@ def main():
     ap.add_argument("--cpu-samples", type=int, default=1 << 22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--pipeline", type=int, default=1,
+                    help="sub-chunks per step: FIR / PSD / xcorr overlap on three HIP streams")
+    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m"):
+        ap.add_argument("--" + k.replace("_", "-"), type=int, default=None)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -136,7 +140,14 @@ def main():
 
     n = args.samples
     taps, pre, tmpl = design(args.ntaps, args.template)
-    cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl)
+    from vector_amd._lib import get_context
+    ctx0 = get_context(local)
+    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m"):
+        v = getattr(args, k)
+        if v is not None:
+            ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, k.encode(), v), k)
+    cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl,
+                      pipeline=args.pipeline)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)
     N = world * n
@@ -218,7 +229,8 @@ def main():
                                 f"{args.template}-sample template xcorr (valid) + argmax"),
                    "samples_per_gpu": n, "total_samples": N, "ntaps": args.ntaps,
                    "decim": args.decim, "nfft": args.nfft, "template": args.template,
-                   "parallelism": f"time-chunk x{world} (RCCL halos)"},
+                   "parallelism": f"time-chunk x{world} (RCCL halos)",
+                   "pipeline": args.pipeline},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},

@@ -24,7 +24,7 @@ class OracleBackend:
         return torch.zeros(n, dtype=dtype)
 
     def fir_into(self, x_ext, nhist, y):
-        x = x_ext.numpy()
+        x = x_ext.contiguous().numpy()
         full = np.convolve(x, self.cfg.taps)[nhist: len(x)]
         y.copy_(torch.from_numpy(full[:: self.cfg.decim].astype(np.complex64)))
 
@@ -32,14 +32,13 @@ class OracleBackend:
         _, _, S = ref.spectrum(y.numpy(), 1.0, "hann", self.cfg.nfft, 0, self.cfg.nfft)
         sxx.copy_(torch.from_numpy(np.ascontiguousarray(S.T).ravel()))
 
-    def xcorr_peak(self, s):
+    def xcorr_peak(self, s, rec):
         c = np.correlate(s.numpy().astype(np.complex128),
                          self.cfg.template.astype(np.complex128), "valid")
         a = np.abs(c)
         i = int(np.argmax(a))
-        rec = torch.tensor([a[i], 0.0, a.sum(), (a * a).sum()], dtype=torch.float64)
+        rec.copy_(torch.tensor([a[i], 0.0, a.sum(), (a * a).sum()], dtype=torch.float64))
         rec.view(torch.int64)[1] = i
-        return rec
 
 
 def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
@@ -48,19 +47,21 @@ def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
     x = ref.synth_iq(N, seed=world)
     taps = rng.standard_normal(ntaps).astype(np.float32)
     pre = ref.qpsk_preamble(L, seed=7)
-    k0 = k0 if k0 is not None else n_local // decim - L // 2     # straddles the first boundary
+    if k0 is None:   # straddles the first rank boundary (or a sub-chunk boundary on 1 rank)
+        k0 = n_local // decim - L // 2 if world > 1 else n_local // decim // 4 - L // 2
     y_full = np.convolve(x, taps)[:N][::decim].astype(np.complex64)
     y_full[k0:k0 + L] += 6 * pre                                   # plant after filtering
     return x, taps, pre, k0, y_full
 
 
-def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q):
+def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from vector_amd.shard import ChainConfig, StreamChain
         x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L)
-        cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre)
+        cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre,
+                          pipeline=pipeline)
         be = OracleBackend(cfg)
 
         class PlantingBackend(OracleBackend):
@@ -68,14 +69,18 @@ def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q):
             single-stream reference does) before the PSD / xcorr stages."""
             def fir_into(self, x_ext, nhist, y):
                 super().fir_into(x_ext, nhist, y)
-                ny = y.shape[0]
-                lo, hi = rank * ny, (rank + 1) * ny
+                nyk = y.shape[0]
+                start = (y.data_ptr() - ch_holder[0].y_ext.data_ptr()) // 8   # sub-chunk offset
+                lo = rank * (n_local // decim) + start
+                hi = lo + nyk
                 a, b = max(lo, k0), min(hi, k0 + L)
                 if a < b:
                     y[a - lo:b - lo] += torch.from_numpy((6 * pre[a - k0:b - k0]).astype(np.complex64))
 
+        ch_holder = []
         be = PlantingBackend(cfg)
         ch = StreamChain(cfg, be, rank, world)
+        ch_holder.append(ch)
         ch.x.copy_(torch.from_numpy(x[rank * n_local:(rank + 1) * n_local]))
         ch.step()
         q.put((rank, ch.y.numpy().copy(), ch.sxx.numpy().copy(), ch.global_peak()))
@@ -91,13 +96,14 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_chain_matches_single_stream(world):
+@pytest.mark.parametrize("world,pipeline", [(2, 1), (3, 1), (2, 4), (1, 4)])
+def test_sharded_chain_matches_single_stream(world, pipeline):
     n_local, decim, nfft, ntaps, L = 4096, 2, 256, 31, 100
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n_local, decim, nfft, ntaps, L, q))
+    procs = [ctx.Process(target=_worker,
+                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -32,7 +32,7 @@ def main():
     lib, h = ctx.lib, ctx.h
     dev = "cuda:0"
     g = torch.Generator(device=dev).manual_seed(1)
-    x = torch.randn(n + 255, dtype=torch.complex64, device=dev, generator=g)
+    x = torch.randn(n + 254, dtype=torch.complex64, device=dev, generator=g)
     y = torch.empty(n, dtype=torch.complex64, device=dev)
     sxx = torch.empty(n, dtype=torch.float32, device=dev)
     import scipy.signal
@@ -44,11 +44,11 @@ def main():
     pk = torch.zeros(4, dtype=torch.float64, device=dev)
 
     cases = []
-    for v in (0, 1):
+    for v in (0, 8):
         cases.append(("psd", v, 8192))
-    for v, m in itertools.product((0, 1), (4096, 8192)):
+    for v, m in itertools.product((0, 8), (4096, 8192)):
         cases.append(("fir", v, m))
-    for v, m in itertools.product((0, 1, 2, 3), (8192, 16384)):
+    for v, m in itertools.product((0, 2, 8, 10), (8192, 16384)):
         if m == 8192 and v & 2:
             continue
         cases.append(("xcorr", v, m))
@@ -66,7 +66,7 @@ def main():
         elif kind == "fir":
             lib.vsig_set_option(h, b"fir_variant", v)
             f = objs[("fir", m)]
-            f(x, out=y, nhist=255 - 1)
+            f(x, out=y, nhist=254)
         else:
             lib.vsig_set_option(h, b"xcorr_variant", v)
             xc = objs[("xcorr", m)]

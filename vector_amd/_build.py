@@ -31,6 +31,7 @@ def build(force: bool = False, verbose: bool = True) -> str:
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     tmp = LIB + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-fno-slp-vectorize",   # SLP packs f32 pairs into v_pk_* + v_mov shuffles
            "-Wall", "-Wno-unused-function",
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
     if verbose:

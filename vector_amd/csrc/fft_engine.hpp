@@ -137,6 +137,13 @@ struct Plan {
 
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
+// 0, but unknown to the optimiser (blocks CSE / LICM across FFT calls).
+__device__ __forceinline__ int opaque_zero() {
+  int z = 0;
+  asm volatile("" : "+s"(z));
+  return z;
+}
+
 // Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E).
 template <int I> struct IC { static constexpr int value = I; };
 template <int B, int E, class F>
@@ -154,6 +161,22 @@ __device__ __forceinline__ void static_for(F&& f) {
 //             retired in issue order).
 struct TwTable { const float2* tw; };
 struct TwAnchors { const float2* wa; };
+//  TwLds    : a two-level table in LDS, W_N^m = A[m >> S] * B[m & (2^S - 1)]
+//             (S = ceil(log2 N / 2); <= 256 entries, 2 KB), filled once per
+//             block from global memory: LDS latency instead of an L2 round
+//             trip per pass, one extra complex multiply per twiddle.
+struct TwLds { const float2* t2; };
+
+constexpr int ilog2c(int n) { int l = 0; while ((1 << l) < n) ++l; return l; }
+template <class P> constexpr int tw2_shift() { return (ilog2c(P::N) + 1) / 2; }
+template <class P> constexpr int tw2_hi() { return P::N >> tw2_shift<P>(); }
+template <class P> constexpr int tw2_size() { return tw2_hi<P>() + (1 << tw2_shift<P>()); }
+
+// Copy the global two-level table (A then B, built on the host) into LDS.
+template <class P>
+__device__ __forceinline__ void load_tw2(float2* t2, const float2* __restrict__ g, int tid, int nthreads) {
+  for (int i = tid; i < tw2_size<P>(); i += nthreads) t2[i] = g[i];
+}
 
 template <class P>
 constexpr int nanch(int p) { return 1 + (P::R[p] - 1) / 8; }
@@ -184,34 +207,68 @@ __device__ __forceinline__ void load_anchors(float2* wa, const float2* __restric
   });
 }
 
-// stage p: twiddle (p > 0) + register DFT for each of this thread's butterflies
+// stage p: twiddle (p > 0) + register DFT for each of this thread's butterflies.
+// hook() runs in the last pass after all of its twiddle loads have been issued
+// and consumed, before the DFTs: a persistent kernel issues its next-unit
+// prefetch there, so no later load in the unit has to wait behind it.
+struct NoHook { __device__ __forceinline__ void operator()() const {} };
+
 template <class P, int p, class TW>
-__device__ __forceinline__ void fft_stage(float2* v, TW tws, int t) {
+__device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
-  constexpr int B = P::E / R;
+  if constexpr (std::is_same<TW, TwTable>::value) {
+    const unsigned j = (unsigned)t + b * P::TF;
+    const unsigned k = j & (Ns - 1);
+    const float2* twp = tws.tw + P::twoff(p);
 #pragma unroll
-  for (int b = 0; b < B; ++b) {
-    if constexpr (p > 0) {
-      if constexpr (std::is_same<TW, TwTable>::value) {
-        const int j = t + b * P::TF;
-        const int k = j & (Ns - 1);
-        const float2* twp = tws.tw + P::twoff(p) + k;
+    for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], twp[k + (unsigned)((r - 1) * Ns)]);
+  } else if constexpr (std::is_same<TW, TwLds>::value) {
+    constexpr int S = tw2_shift<P>();
+    constexpr int stride = P::N / (Ns * R);       // W_{Ns R}^{rk} = W_N^{rk stride}
+    const int j = t + b * P::TF;
+    const int k = j & (Ns - 1);
+    const float2* A = tws.t2;
+    const float2* Bt = tws.t2 + tw2_hi<P>();
 #pragma unroll
-        for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], twp[(r - 1) * Ns]);
-      } else {
-        constexpr int NA = nanch<P>(p);
-        const float2* wa = tws.wa + anch_off<P>(p) + b * NA;
-        const float2 w1 = wa[0];
-        float2 cur = w1;
-#pragma unroll
-        for (int r = 1; r < R; ++r) {
-          if (r > 1) cur = (r % 8 == 0) ? wa[r / 8] : cmul(cur, w1);
-          v[b * R + r] = cmul(v[b * R + r], cur);
-        }
-      }
+    for (int r = 1; r < R; ++r) {
+      const int m = k * (r * stride);
+      const float2 w = cmul(A[m >> S], Bt[m & ((1 << S) - 1)]);
+      v[b * R + r] = cmul(v[b * R + r], w);
     }
-    dft_reg<R>(v + b * R);
+  } else {
+    constexpr int NA = nanch<P>(p);
+    const float2* wa = tws.wa + anch_off<P>(p) + b * NA;
+    const float2 w1 = wa[0];
+    float2 cur = w1;
+#pragma unroll
+    for (int r = 1; r < R; ++r) {
+      if (r > 1) cur = (r % 8 == 0) ? wa[r / 8] : cmul(cur, w1);
+      v[b * R + r] = cmul(v[b * R + r], cur);
+    }
+  }
+}
+
+template <class P, int p, class TW, class H = NoHook>
+__device__ __forceinline__ void fft_stage(float2* v, TW tws, int t, H hook = H{}) {
+  constexpr int R = P::R[p];
+  constexpr int B = P::E / R;
+  if constexpr (p == P::NP - 1 && !std::is_same<H, NoHook>::value) {
+    if constexpr (p > 0) {
+#pragma unroll
+      for (int b = 0; b < B; ++b) fft_twiddle<P, p>(v, tws, t, b);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    hook();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int b = 0; b < B; ++b) dft_reg<R>(v + b * R);
+  } else {
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+      if constexpr (p > 0) fft_twiddle<P, p>(v, tws, t, b);
+      dft_reg<R>(v + b * R);
+    }
   }
 }
 
@@ -255,15 +312,15 @@ __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   });
 }
 
-template <class P, int p, class TW>
-__device__ __forceinline__ void fft_tail(float2* v, float2* lds, TW tws, int t) {
+template <class P, int p, class TW, class H = NoHook>
+__device__ __forceinline__ void fft_tail(float2* v, float2* lds, TW tws, int t, H hook = H{}) {
   if constexpr (p < P::NP) {
     __syncthreads();               // previous readers of lds are done
     fft_store<P, p - 1>(v, lds, t);
     __syncthreads();
     fft_load<P, p>(v, lds, t);
-    fft_stage<P, p>(v, tws, t);
-    fft_tail<P, p + 1>(v, lds, tws, t);
+    fft_stage<P, p>(v, tws, t, hook);
+    fft_tail<P, p + 1>(v, lds, tws, t, hook);
   }
 }
 
@@ -273,10 +330,11 @@ __device__ __forceinline__ void fft_tail(float2* v, float2* lds, TW tws, int t) 
 template <class P>
 __device__ __forceinline__ void fft_frame(float2* v, float2* lds, const float2* tw, int t) {
   static_assert(P::valid(), "invalid FFT plan");
-  // Launder the table pointer: a kernel running two FFTs (overlap-save) would
+  // Launder the table offset: a kernel running two FFTs (overlap-save) would
   // otherwise have its twiddle loads CSE'd across them and keep every twiddle
-  // of the first FFT live in VGPRs until the second.
-  asm volatile("" : "+s"(tw));
+  // of the first FFT live in VGPRs until the second.  (An opaque zero offset,
+  // not the pointer itself, so the loads stay global_load, not flat_load.)
+  tw += opaque_zero();
   fft_stage<P, 0>(v, TwTable{tw}, t);
   fft_tail<P, 1>(v, lds, TwTable{tw}, t);
 }
@@ -288,6 +346,24 @@ template <class P>
 __device__ __forceinline__ void launder_anchors(float2* wa) {
 #pragma unroll
   for (int i = 0; i < nanch_total<P>(); ++i) asm volatile("" : "+v"(wa[i].x), "+v"(wa[i].y));
+}
+
+// Two-level LDS twiddles (see TwLds); t2 must be filled before the call.
+template <class P>
+__device__ __forceinline__ void fft_frame_t2(float2* v, float2* lds, const float2* t2, int t) {
+  static_assert(P::valid(), "invalid FFT plan");
+  fft_stage<P, 0>(v, TwLds{t2}, t);
+  fft_tail<P, 1>(v, lds, TwLds{t2}, t);
+}
+
+// Table twiddles + a hook in the last pass (see fft_stage).
+template <class P, class H>
+__device__ __forceinline__ void fft_frame_hook(float2* v, float2* lds, const float2* tw, int t,
+                                               H hook) {
+  static_assert(P::valid(), "invalid FFT plan");
+  tw += opaque_zero();
+  fft_stage<P, 0>(v, TwTable{tw}, t, hook);
+  fft_tail<P, 1>(v, lds, TwTable{tw}, t, hook);
 }
 
 // The same with register-resident twiddle anchors (see TwAnchors).

@@ -45,12 +45,36 @@ __global__ __launch_bounds__(block_threads<P>()) void psd_kernel(
     const float2* __restrict__ tw) {
   constexpr int BT = block_threads<P>();
   constexpr int FPB = BT / P::TF;
-  __shared__ float2 lds[FPB * P::LDS];
+  __shared__ float2 lds[FPB * P::LDS + (PERSIST == 3 ? tw2_size<P>() : 0)];
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
   const long long units = (nframes + FPB - 1) / FPB;
   long long u = blockIdx.x;
   if (u >= units) return;
+  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
+    float2* t2 = lds + FPB * P::LDS;
+    load_tw2<P>(t2, tw, threadIdx.x, BT);
+    float2 v[P::E];
+    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = in_index<P>(t, e);
+      const float w = i < nperseg ? win[i] : 0.f;
+      v[e] = make_float2(v[e].x * w, v[e].y * w);
+    }
+    fft_frame_t2<P>(v, lds + fl * P::LDS, t2, t);
+    const long long frame = u * FPB + fl;
+    if (frame < nframes) {
+      float* of = out + frame * P::N;
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = out_index<P>(t, e);
+        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+      }
+    }
+    return;
+  }
 
   if constexpr (!PERSIST) {          // one unit per block, table twiddles
     float2 v[P::E];
@@ -71,6 +95,35 @@ __global__ __launch_bounds__(block_threads<P>()) void psd_kernel(
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
         of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
       }
+    }
+    return;
+  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
+    float2 v[P::E];
+    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
+    for (; u < units; u += gridDim.x) {
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = in_index<P>(t, e);
+        const float w = i < nperseg ? win[i] : 0.f;
+        v[e] = make_float2(v[e].x * w, v[e].y * w);
+      }
+      float2 nv[P::E];
+      const long long nu = u + gridDim.x;
+      fft_frame_hook<P>(v, lds + fl * P::LDS, tw, t, [&] {
+        if (nu < units) psd_load<P>(nv, x, stride, nperseg, hop, nu * FPB + fl, nframes, t);
+      });
+      const long long frame = u * FPB + fl;
+      if (frame < nframes) {
+        float* of = out + frame * P::N;
+#pragma unroll
+        for (int e = 0; e < P::E; ++e) {
+          const int i = out_index<P>(t, e);
+          const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+          of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+        }
+      }
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
     }
     return;
   }
@@ -143,13 +196,39 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
   const float2* base = x + s0;
   if (s0 >= 0 && s0 + P::N <= n) {
 #pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = base[in_index<P>(t, e)];
+    for (int e = 0; e < P::E; ++e) v[e] = base[(unsigned)in_index<P>(t, e)];
   } else {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = in_index<P>(t, e);
       const long long xi = s0 + i;
       v[e] = (xi >= 0 && xi < n) ? base[i] : make_float2(0.f, 0.f);
+    }
+  }
+}
+
+// Store the valid outputs of FIR block b (conj undoes the inverse-by-conj
+// trick): block-local 32-bit offsets from a per-block base; hop is a multiple
+// of decim, so the decimation phase is the local index's.
+template <class P>
+__device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ y, long long b,
+                                          long long hop, int lo, long long nloc, int decim, int t) {
+  const long long gb = b * hop;
+  const long long rem = nloc - gb;
+  const int lim = rem < hop ? (int)rem : (int)hop;
+  if (decim == 1) {
+    float2* yb = y + gb;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e) - lo;
+      if (i >= 0 && i < lim) yb[(unsigned)i] = cconj(v[e]);
+    }
+  } else {
+    float2* yb = y + gb / decim;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e) - lo;
+      if (i >= 0 && i < lim && i % decim == 0) yb[(unsigned)(i / decim)] = cconj(v[e]);
     }
   }
 }
@@ -170,13 +249,25 @@ __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   constexpr int BT = block_threads<P>();
   static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[P::LDS];
+  __shared__ float2 lds[P::LDS + (PERSIST == 3 ? tw2_size<P>() : 0)];
   const int t = threadIdx.x;
   long long b = blockIdx.x;
   if (b >= nblocks) return;  // uniform per block
 
   const int lo = ntaps - 1;
   const long long nloc = n - g0;
+  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
+    float2* t2 = lds + P::LDS;
+    load_tw2<P>(t2, tw, t, BT);
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame_t2<P>(v, lds, t2, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame_t2<P>(v, lds, t2, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  }
   if constexpr (!PERSIST) {          // one unit per block, table twiddles
     float2 v[P::E];
     load_segment<P>(v, x, g0 + b * hop - lo, n, t);
@@ -184,12 +275,23 @@ __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
 #pragma unroll
     for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
     fft_frame<P>(v, lds, tw, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    for (; b < nblocks; b += gridDim.x) {
+      fft_frame<P>(v, lds, tw, t);
 #pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const int i = out_index<P>(t, e) - lo;
-      const long long g = b * hop + i;
-      if (i >= 0 && i < hop && g < nloc && (decim == 1 || g % decim == 0))
-        y[decim == 1 ? g : g / decim] = cconj(v[e]);
+      for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+      float2 nv[P::E];
+      const long long nb = b + gridDim.x;
+      fft_frame_hook<P>(v, lds, tw, t, [&] {
+        if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
+      });
+      fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
     }
     return;
   }
@@ -207,13 +309,7 @@ __global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
     const long long nb = b + gridDim.x;
     if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
     fft_frame_anch<P>(v, lds, wa, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const int i = out_index<P>(t, e) - lo;
-      const long long g = b * hop + i;          // output index relative to g0
-      if (i >= 0 && i < hop && g < nloc && (decim == 1 || g % decim == 0))
-        y[decim == 1 ? g : g / decim] = cconj(v[e]);
-    }
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
 #pragma unroll
     for (int e = 0; e < P::E; ++e) v[e] = nv[e];
   }
@@ -267,24 +363,26 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
                                                long long nout, float2* __restrict__ c,
                                                int store_mode, PeakPartial* partials, int t) {
   constexpr int BT = block_threads<P>();
+  const long long ob = b * hop;                         // block's first output
+  const long long rem = nout - ob;
+  const int lim = rem < hop ? (int)rem : (int)hop;
   float m = -1.f;
-  long long mi = 0x7fffffffffffffffLL;
+  int mi = 0x7fffffff;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = out_index<P>(t, e);
-    const long long o = b * hop + i;
-    if (i < hop && o < nout) {
+    if (i < lim) {
       const float2 cv = cconj(v[e]);
       const float a2 = cv.x * cv.x + cv.y * cv.y;
-      better(m, mi, a2, o);
+      if (a2 > m || (a2 == m && i < mi)) { m = a2; mi = i; }
       s1 += sqrtf(a2);
       s2 += a2;
-      if (store_mode == 1) c[o] = cv;
-      else if (store_mode == 2) c[nout - 1 - o] = cconj(cv);
+      if (store_mode == 1) (c + ob)[(unsigned)i] = cv;
+      else if (store_mode == 2) (c + (nout - 1 - ob))[-i] = cconj(cv);
     }
   }
-  if (partials) block_partial<BT>((double)m, mi, (double)s1, (double)s2, partials + b);
+  if (partials) block_partial<BT>((double)m, ob + mi, (double)s1, (double)s2, partials + b);
 }
 
 template <class P, int PERSIST>
@@ -295,11 +393,23 @@ __global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   constexpr int BT = block_threads<P>();
   static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[P::LDS];
+  __shared__ float2 lds[P::LDS + (PERSIST == 3 ? tw2_size<P>() : 0)];
   const int t = threadIdx.x;
   long long b = blockIdx.x;
   if (b >= nblocks) return;
 
+  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
+    float2* t2 = lds + P::LDS;
+    load_tw2<P>(t2, tw, t, BT);
+    float2 v[P::E];
+    load_segment<P>(v, s, b * hop - off, n, t);
+    fft_frame_t2<P>(v, lds, t2, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+    fft_frame_t2<P>(v, lds, t2, t);
+    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+    return;
+  }
   if constexpr (!PERSIST) {          // one unit per block, table twiddles
     float2 v[P::E];
     load_segment<P>(v, s, b * hop - off, n, t);
@@ -308,6 +418,23 @@ __global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
     for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
     fft_frame<P>(v, lds, tw, t);
     xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+    return;
+  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
+    float2 v[P::E];
+    load_segment<P>(v, s, b * hop - off, n, t);
+    for (; b < nblocks; b += gridDim.x) {
+      fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+      float2 nv[P::E];
+      const long long nb = b + gridDim.x;
+      fft_frame_hook<P>(v, lds, tw, t, [&] {
+        if (nb < nblocks) load_segment<P>(nv, s, nb * hop - off, n, t);
+      });
+      xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
+    }
     return;
   }
   float2 wa[nanch_total<P>()];
@@ -422,7 +549,8 @@ void launch_psd_t(const float2* x, long long stride, const float* win, int npers
   constexpr int BT = block_threads<PL>();
   constexpr int FPB = BT / PL::TF;
   const long long units = (nframes + FPB - 1) / FPB;
-  const long long grid = PERSIST ? persistent_grid(psd_kernel<PL, 1>, BT, units) : units;
+  const long long grid =
+      (PERSIST == 1 || PERSIST == 2) ? persistent_grid(psd_kernel<PL, PERSIST>, BT, units) : units;
   hipLaunchKernelGGL((psd_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(BT), 0, st, x, stride,
                      win, nperseg, hop, scale, out, nframes, shift, tw);
 }
@@ -432,7 +560,9 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                       const float2* tw, int variant, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
   VSIG_PLAN_SWITCH(N, {
-    if (variant & 1) launch_psd_t<PL, 1>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    if (variant & 8) launch_psd_t<PL, 3>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    else if (variant & 4) launch_psd_t<PL, 2>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    else if (variant & 1) launch_psd_t<PL, 1>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else launch_psd_t<PL, 0>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
   });
   return hipGetLastError();
@@ -467,7 +597,8 @@ void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, 
                   long long hop, int decim, float2* y, long long nblocks, const float2* tw,
                   hipStream_t st) {
   const long long grid =
-      PERSIST ? persistent_grid(fir_os_kernel<PL, 1>, block_threads<PL>(), nblocks) : nblocks;
+      (PERSIST == 1 || PERSIST == 2)
+          ? persistent_grid(fir_os_kernel<PL, PERSIST>, block_threads<PL>(), nblocks) : nblocks;
   hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(block_threads<PL>()),
                      0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
 }
@@ -478,7 +609,9 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
   VSIG_OS_SWITCH(M, variant, {
-    if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 4) launch_fir_t<PL, 2>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else launch_fir_t<PL, 0>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
   });
   return hipGetLastError();
@@ -489,7 +622,8 @@ void launch_xcorr_t(const float2* s, long long n, const float2* Ps, long long of
                     long long hop, float2* c, int store_mode, PeakPartial* partials,
                     long long nblocks, const float2* tw, hipStream_t st) {
   const long long grid =
-      PERSIST ? persistent_grid(xcorr_os_kernel<PL, 1>, block_threads<PL>(), nblocks) : nblocks;
+      (PERSIST == 1 || PERSIST == 2)
+          ? persistent_grid(xcorr_os_kernel<PL, PERSIST>, block_threads<PL>(), nblocks) : nblocks;
   hipLaunchKernelGGL((xcorr_os_kernel<PL, PERSIST>), dim3((unsigned)grid),
                      dim3(block_threads<PL>()), 0, st, s, n, Ps, off, nout, hop, c, store_mode,
                      partials, nblocks, tw);
@@ -501,7 +635,9 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
   VSIG_OS_SWITCH(M, variant, {
-    if (variant & 1) launch_xcorr_t<PL, 1>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+    if (variant & 8) launch_xcorr_t<PL, 3>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+    else if (variant & 4) launch_xcorr_t<PL, 2>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+    else if (variant & 1) launch_xcorr_t<PL, 1>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
     else launch_xcorr_t<PL, 0>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
   });
   return hipGetLastError();
@@ -528,6 +664,12 @@ hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, i
 }  // namespace vsig
 
 namespace vsig {
+hipError_t tw2_info(int N, int* shift, int* hi) {
+  if (N == -16384) { *shift = tw2_shift<Plan16384w>(); *hi = tw2_hi<Plan16384w>(); return hipSuccess; }
+  VSIG_PLAN_SWITCH(N, { *shift = tw2_shift<PL>(); *hi = tw2_hi<PL>(); });
+  return hipSuccess;
+}
+
 hipError_t plan_info(int N, int* radices, int* npasses) {
   if (N == -16384) {   // the E = 32 plan of 16384 points (variant bit 1)
     *npasses = Plan16384w::NP;

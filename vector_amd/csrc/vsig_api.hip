@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{1, 0, 0};           // tuned defaults (see vsig_set_option)
+  vsig::Variants var{8, 8, 10};         // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
 };
 
@@ -91,6 +91,38 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
 }
 
 int tw_key(int M, int variant) { return (M == 16384 && (variant & 2)) ? -16384 : M; }
+
+// Two-level table for plan key N (cached under key N + 2^20).
+int get_tw2(vsig_ctx* c, int N, const float2** out) {
+  const int key = N + (1 << 20);
+  auto it = c->tw.find(key);
+  if (it != c->tw.end()) { *out = it->second; return VSIG_OK; }
+  int S = 0, hi = 0;
+  if (vsig::tw2_info(N, &S, &hi) != hipSuccess)
+    return fail(c, VSIG_E_UNSUPPORTED, "FFT size " + std::to_string(N) + " not supported");
+  const int n = N < 0 ? -N : N;
+  std::vector<float2> h;
+  for (int i = 0; i < hi; ++i) {
+    const double a = -2.0 * M_PI * (double)i * (double)(1 << S) / (double)n;
+    h.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+  }
+  for (int i = 0; i < (1 << S); ++i) {
+    const double a = -2.0 * M_PI * (double)i / (double)n;
+    h.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+  }
+  float2* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, h.size() * sizeof(float2)));
+  HIPCHK(c, hipMemcpy(d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice));
+  c->tw[key] = d;
+  *out = d;
+  return VSIG_OK;
+}
+
+// Twiddle operand of a launch: the per-pass table, or (variant bit 3) the
+// two-level table.
+int get_tw_for(vsig_ctx* c, int M, int variant, const float2** out) {
+  return (variant & 8) ? get_tw2(c, tw_key(M, variant), out) : get_twiddles(c, tw_key(M, variant), out);
+}
 
 int ensure_partials(vsig_ctx* c, long long n) {
   if (n <= c->npartials) return VSIG_OK;
@@ -194,7 +226,7 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, int L, const float2* s, long
   int rc = ensure_partials(c, nblocks);
   if (rc) return rc;
   const float2* tw;
-  rc = get_twiddles(c, tw_key(M, c->var.xcorr), &tw);
+  rc = get_tw_for(c, M, c->var.xcorr, &tw);
   if (rc) return rc;
   {
     Timed t(c, "xcorr");
@@ -273,9 +305,9 @@ int vsig_set_stream(vsig_ctx* c, void* s) {
 int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   if (!c || !key) return VSIG_E_INVALID;
   const std::string k(key);
-  if (k == "psd_variant") c->var.psd = value & 1;
-  else if (k == "fir_variant") c->var.fir = value & 3;
-  else if (k == "xcorr_variant") c->var.xcorr = value & 3;
+  if (k == "psd_variant") c->var.psd = value & 13;
+  else if (k == "fir_variant") c->var.fir = value & 15;
+  else if (k == "xcorr_variant") c->var.xcorr = value & 15;
   else if (k == "fir_m" || k == "xcorr_m") {
     if (value != 0 && value != 4096 && value != 8192 && value != 16384)
       return fail(c, VSIG_E_INVALID, "block size must be 0, 4096, 8192 or 16384");
@@ -326,7 +358,7 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
     return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
   const float2* tw;
-  int rc = get_twiddles(c, nfft, &tw);
+  int rc = get_tw_for(c, nfft, c->var.psd & 8, &tw);
   if (rc) return rc;
   Timed t(c, "psd");
   HIPCHK(c, vsig::launch_psd(nfft, (const float2*)x, stride, win, nperseg, hop, scale, sxx, nframes,
@@ -390,7 +422,7 @@ int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n,
   if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
-  int rc = get_twiddles(c, tw_key(f->M, c->var.fir), &tw);
+  int rc = get_tw_for(c, f->M, c->var.fir, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,

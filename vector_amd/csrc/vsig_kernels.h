@@ -16,8 +16,13 @@ struct PeakPartial {
 
 // Radices of the plan for N points (N = -16384: the E = 32 plan of 16384).
 hipError_t plan_info(int N, int* radices, int* npasses);
+// Two-level twiddle table geometry: W_N^m = A[m >> shift] * B[m & (2^shift - 1)],
+// A has `hi` entries, B has 2^shift.
+hipError_t tw2_info(int N, int* shift, int* hi);
 
-// Kernel variants (tuning): bit 0 persistent; bit 1 (M = 16384) E = 32 plan.
+// Kernel variants (tuning): bit 0 persistent + register twiddle anchors;
+// bit 1 (M = 16384) E = 32 plan; bit 2 persistent + late prefetch; bit 3
+// two-level LDS twiddle table (one unit per block).
 struct Variants { int psd, fir, xcorr; };
 
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,

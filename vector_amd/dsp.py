@@ -65,6 +65,20 @@ def _ptr(t: torch.Tensor):
     return C.c_void_p(t.data_ptr())
 
 
+def _check_dev(t: torch.Tensor, n: int, dtype, what: str, device=None):
+    """Host-side shape check before a kernel writes / reads a caller buffer."""
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{what}: expected a CUDA tensor")
+    if t.dtype != dtype:
+        raise ValueError(f"{what}: dtype {t.dtype}, expected {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{what}: must be contiguous")
+    if t.numel() < n:
+        raise ValueError(f"{what}: {t.numel()} elements, need {n}")
+    if device is not None and t.device.index != device:
+        raise ValueError(f"{what}: on {t.device}, expected cuda:{device}")
+
+
 def _peak_buffer(ctx):
     return torch.empty(PEAK_BYTES // 8, dtype=torch.float64, device=f"cuda:{ctx.device}")
 
@@ -211,10 +225,14 @@ class FirFilter:
         The first nhist samples of x are history (a left halo): only the
         remaining samples produce outputs."""
         self.ctx.bind_stream()
+        _check_dev(x, 1, torch.complex64, "filter input", self.ctx.device)
         n = int(x.shape[0]) - int(nhist)
+        if n < 1 or nhist < 0:
+            raise ValueError("filter: need len(x) > nhist >= 0")
         ny = self.out_len(n)
         if out is None:
             out = torch.empty(ny, dtype=torch.complex64, device=x.device)
+        _check_dev(out, ny, torch.complex64, "filter output", self.ctx.device)
         self.ctx.check(self.ctx.lib.vsig_fir_exec_hist_dev(self.h, _ptr(x), int(nhist), n,
                                                            _ptr(out), ny), "filter")
         return out
@@ -405,8 +423,18 @@ class Correlator:
                  peak: torch.Tensor | None = None):
         """Enqueue; returns (c or None, peak buffer (device vsig_peak_t))."""
         self.ctx.bind_stream()
+        _check_dev(s, 1, torch.complex64, "correlator stream", self.ctx.device)
+        if mode not in ("valid", "full"):
+            raise ValueError("Correlator supports mode 'valid' and 'full'")
+        ns = int(s.shape[0])
+        nout = ns - self.L + 1 if mode == "valid" else ns + self.L - 1
+        if nout < 1:
+            raise ValueError("stream shorter than the template")
+        if out is not None:
+            _check_dev(out, nout, torch.complex64, "correlator output", self.ctx.device)
         if peak is None:
             peak = _peak_buffer(self.ctx)
+        _check_dev(peak, 4, torch.float64, "peak record", self.ctx.device)
         self.ctx.check(self.ctx.lib.vsig_xcorr_exec_dev(
             self.h, _ptr(s), int(s.shape[0]), _lib.MODES[mode],
             _ptr(out) if out is not None else None, _ptr(peak)), "xcorr")

@@ -25,7 +25,7 @@ unit-tested on CPU with gloo; the product backend is HipBackend (libvsig.so).
 """
 from __future__ import annotations
 
-import math
+import contextlib
 from dataclasses import dataclass
 
 import numpy as np
@@ -43,13 +43,19 @@ class ChainConfig:
     nfft: int = 8192             # PSD frame = hop (non-overlapping)
     template: np.ndarray | None = None   # sync preamble (None: no xcorr stage)
     window: str = "hann"
+    pipeline: int = 1            # sub-chunks per step (FIR / PSD / xcorr overlap on 3 streams)
 
     def validate(self, world: int):
         ny = self.n_local // self.decim
-        if self.n_local % self.decim:
-            raise ValueError("n_local must be a multiple of decim")
-        if ny % self.nfft:
-            raise ValueError("n_local/decim must be a multiple of nfft (frames never straddle chunks)")
+        K = self.pipeline
+        if K < 1 or self.n_local % K:
+            raise ValueError("n_local must be a multiple of pipeline")
+        if self.n_local % (self.decim * K):
+            raise ValueError("n_local must be a multiple of decim * pipeline")
+        if (ny // K) % self.nfft:
+            raise ValueError("n_local/decim/pipeline must be a multiple of nfft (frames never straddle chunks)")
+        if self.template is not None and K > 1 and ny // K < len(self.template) - 1:
+            raise ValueError("sub-chunk shorter than the template halo")
         if self.template is not None and world > 1 and ny < len(self.template) - 1:
             raise ValueError("chunk shorter than the template halo")
         if world > 1 and self.n_local < len(self.taps) - 1:
@@ -86,10 +92,34 @@ class HipBackend:
         self.win = torch.from_numpy(w).to(self.dev)
         self.scale = float(1.0 / float(np.sum(w, dtype=np.float64)) ** 2)
         self.nfft = cfg.nfft
-        self.peak = torch.zeros(4, dtype=torch.float64, device=self.dev)
+        self.lanes = {k: torch.cuda.Stream(device=self.dev) for k in ("fir", "psd", "xcorr")}
 
     def empty(self, n, dtype=torch.complex64):
         return torch.zeros(n, dtype=dtype, device=self.dev)
+
+    # stream "lanes": the three stages of a pipelined step run on their own
+    # HIP streams, ordered by events (FIR(k) -> PSD(k); FIR(k+1) -> xcorr(k)).
+    def lane(self, name):
+        return torch.cuda.stream(self.lanes[name])
+
+    def record(self):
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev
+
+    def wait(self, ev):
+        if ev is not None:
+            torch.cuda.current_stream(self.dev).wait_event(ev)
+
+    def join(self):
+        cur = torch.cuda.current_stream(self.dev)
+        for st in self.lanes.values():
+            cur.wait_stream(st)
+
+    def fork(self):
+        cur = torch.cuda.current_stream(self.dev)
+        for st in self.lanes.values():
+            st.wait_stream(cur)
 
     def fir_into(self, x_ext, nhist, y):
         self.fir(x_ext, out=y, nhist=nhist)
@@ -99,15 +129,29 @@ class HipBackend:
         ctx.bind_stream()
         n = int(y.shape[0])
         nframes = n // self.nfft
+        self.dsp._check_dev(y, n, torch.complex64, "psd input")
+        self.dsp._check_dev(sxx, nframes * self.nfft, torch.float32, "psd output")
         ctx.check(ctx.lib.vsig_psd_c64_dev(ctx.h, self.dsp._ptr(y), n, 1, self.dsp._ptr(self.win),
                                            self.nfft, self.nfft, self.nfft, self.scale, 0,
                                            self.dsp._ptr(sxx), nframes), "psd")
 
-    def xcorr_peak(self, s):
-        """valid correlation over s; returns a device float64[4] record
+    def xcorr_peak(self, s, rec):
+        """valid correlation over s into the device float64[4] record rec
         (max |c|, local index (int64 bits), sum |c|, sum |c|^2)."""
-        self.xc(s, "valid", peak=self.peak)
-        return self.peak
+        self.xc(s, "valid", peak=rec)
+
+
+def _lane(be, name):
+    return be.lane(name) if hasattr(be, "lane") else contextlib.nullcontext()
+
+
+def _record(be):
+    return be.record() if hasattr(be, "record") else None
+
+
+def _wait(be, ev):
+    if hasattr(be, "wait"):
+        be.wait(ev)
 
 
 class StreamChain:
@@ -123,6 +167,7 @@ class StreamChain:
         self.x_ext = backend.empty(self.hist + cfg.n_local)          # [left halo | chunk]
         self.y_ext = backend.empty(self.ny + max(self.L - 1, 0))     # [chunk out | right halo]
         self.sxx = backend.empty((self.ny // cfg.nfft) * cfg.nfft, torch.float32)
+        self.recs = backend.empty(4 * cfg.pipeline, torch.float64).view(cfg.pipeline, 4)
         self.peak_rows = None
 
     @property
@@ -145,36 +190,62 @@ class StreamChain:
                 req.wait()
 
     def step(self):
-        r, w = self.rank, self.world
-        if w > 1 and self.hist > 0:             # 1. left halo of the input
-            n = self.cfg.n_local
-            self._exchange(self.x_ext[n: n + self.hist] if r < w - 1 else None,
-                           r + 1 if r < w - 1 else None,
-                           self.x_ext[: self.hist] if r > 0 else None,
-                           r - 1 if r > 0 else None)
-        self.be.fir_into(self.x_ext, self.hist, self.y)             # 2. FIR (+ decimation)
-        if w > 1 and self.L > 1:                # 3. right halo of the filtered stream
-            self._exchange(self.y_ext[: self.L - 1] if r > 0 else None,
-                           r - 1 if r > 0 else None,
-                           self.y_ext[self.ny: self.ny + self.L - 1] if r < w - 1 else None,
-                           r + 1 if r < w - 1 else None)
-        self.be.psd_into(self.y, self.sxx)                           # 4. PSD
-        if self.L:                                                   # 5. sync correlation
-            rec = self.be.xcorr_peak(self.y_ext[: self.ny + self.yhalo])
-            if w > 1:                                                # 6. global peak
-                rows = [torch.empty_like(rec) for _ in range(w)]
-                dist.all_gather(rows, rec, group=self.group)
+        r, w, K = self.rank, self.world, self.cfg.pipeline
+        be = self.be
+        n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
+        nk, nyk = n // K, ny // K
+        if hasattr(be, "fork"):
+            be.fork()
+        ev_fir, ev_halo = [], None
+        with _lane(be, "fir"):
+            if w > 1 and hist > 0:              # 1. left halo of the input
+                self._exchange(self.x_ext[n: n + hist] if r < w - 1 else None,
+                               r + 1 if r < w - 1 else None,
+                               self.x_ext[: hist] if r > 0 else None,
+                               r - 1 if r > 0 else None)
+            for k in range(K):                  # 2. FIR (+ decimation), sub-chunk k
+                be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
+                            self.y_ext[k * nyk: (k + 1) * nyk])
+                ev_fir.append(_record(be))
+                if k == 0 and w > 1 and L > 1:  # 3. right halo of the filtered stream
+                    self._exchange(self.y_ext[: L - 1] if r > 0 else None,
+                                   r - 1 if r > 0 else None,
+                                   self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
+                                   r + 1 if r < w - 1 else None)
+                    ev_halo = _record(be)
+        for k in range(K):
+            with _lane(be, "psd"):              # 4. PSD of sub-chunk k
+                _wait(be, ev_fir[k])
+                be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
+            if L:                               # 5. sync correlation of sub-chunk k
+                with _lane(be, "xcorr"):
+                    last = k == K - 1
+                    _wait(be, ev_fir[k + 1] if not last else ev_fir[k])
+                    if last and ev_halo is not None:
+                        _wait(be, ev_halo)
+                    halo = (L - 1) if (not last or r < w - 1) else 0
+                    be.xcorr_peak(self.y_ext[k * nyk: (k + 1) * nyk + halo], self.recs[k])
+        if hasattr(be, "join"):
+            be.join()
+        if L:
+            if w > 1:                           # 6. global peak records
+                rows = [torch.empty_like(self.recs) for _ in range(w)]
+                dist.all_gather(rows, self.recs, group=self.group)
                 self.peak_rows = rows
             else:
-                self.peak_rows = [rec]
+                self.peak_rows = [self.recs]
 
     def global_peak(self):
         """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step."""
         rows = []
+        nyk = self.ny // self.cfg.pipeline
         for r, t in enumerate(self.peak_rows):
-            h = t.detach().cpu()
-            idx = int(h.view(torch.int64)[1].item())
-            rows.append((float(h[0]), r * self.ny + idx, float(h[2]), float(h[3])))
+            h = t.detach().cpu().reshape(-1, 4)
+            hi = h.view(torch.int64)
+            for k in range(h.shape[0]):
+                idx = int(hi[k, 1].item())
+                rows.append((float(h[k, 0]), r * self.ny + k * nyk + idx, float(h[k, 2]),
+                             float(h[k, 3])))
         m, i, s1, s2 = combine_peaks(np.array(rows, dtype=object))
         nout = self.world * self.ny - self.L + 1
         return m, i, s1, s2, nout
