@@ -265,3 +265,39 @@ def test_correlator_stream_full_size_property(gpu):
     assert idx == k0
     direct = abs(np.vdot(pre.astype(np.complex128), s[k0:k0 + L].cpu().numpy().astype(np.complex128)))
     assert peak == pytest.approx(direct, rel=1e-5)
+
+
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18])
+def test_kernel_variants_agree_with_oracle(gpu, variant):
+    """Every tuning variant (persistent / LDS twiddles / split exchange /
+    512-thread 16k plan) must give the same results as the oracle."""
+    ctx = gpu.get_context()
+    rng = np.random.default_rng(variant)
+    x = ref.synth_iq(3 * 16384 + 77, seed=variant)
+    taps = rng.standard_normal(255).astype(np.float32)
+    tmpl = ref.qpsk_preamble(4096, seed=variant)
+    try:
+        for k in ("psd_variant", "fir_variant", "xcorr_variant"):
+            ctx.check(ctx.lib.vsig_set_option(ctx.h, k.encode(), variant), k)
+        for m in (4096, 8192, 16384):
+            ctx.check(ctx.lib.vsig_set_option(ctx.h, b"fir_m", m), "fir_m")
+            gpu.dsp._fir_cache.clear()
+            assert_normwise(gpu.filter(x, taps, 1), ref.fir_filter(x, taps, 1), FIR_TOL)
+            assert_normwise(gpu.filter(x, taps, 3), ref.fir_filter(x, taps, 3), FIR_TOL)
+        for nfft in (1024, 8192, 16384):
+            _, _, S = gpu.spectrum(x, 1.0, "hann", nfft, nfft // 4, nfft)
+            _, _, R = ref.spectrum(x, 1.0, "hann", nfft, nfft // 4, nfft)
+            assert_spectra_close(S, R)
+        for m in (8192, 16384):
+            ctx.check(ctx.lib.vsig_set_option(ctx.h, b"xcorr_m", m), "xcorr_m")
+            c, _ = gpu.cross_correlate_signals(tmpl, x, "valid")
+            r, _ = ref.cross_correlate_signals(tmpl, x, "valid")
+            assert_normwise(c, r, XC_TOL)
+    finally:
+        lib, h = ctx.lib, ctx.h
+        lib.vsig_set_option(h, b"psd_variant", 8)
+        lib.vsig_set_option(h, b"fir_variant", 8)
+        lib.vsig_set_option(h, b"xcorr_variant", 10)
+        lib.vsig_set_option(h, b"fir_m", 0)
+        lib.vsig_set_option(h, b"xcorr_m", 0)
+        gpu.dsp._fir_cache.clear()

@@ -6,6 +6,7 @@ own Python call signatures (utils.py).  No CPU fallback: without the library or
 a HIP device every call raises ``VsigUnavailable``.
 """
 from ._lib import VsigError, VsigUnavailable, get_context, load_library  # noqa: F401
+from . import dsp  # noqa: F401
 from .dsp import (Correlator, FirFilter, correlate, correlate_peak,  # noqa: F401
                   cross_correlate_signals, filter, find_correlation_peak,
                   find_packet_location_in_vector, fir_filter, peak_stats, spectrum)

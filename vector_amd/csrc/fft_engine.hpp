@@ -312,6 +312,65 @@ __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   });
 }
 
+// Split exchange: real and imaginary parts go through an LDS buffer of N
+// floats in two rounds (4 barriers instead of 2), halving the LDS a frame
+// needs so two 16384-point blocks fit on one CU.
+template <class P, int p, int C>
+__device__ __forceinline__ void fft_store_c(const float2* v, float* lds, int t) {
+  constexpr int R = P::R[p];
+  constexpr int Ns = P::ns(p);
+  constexpr int B = P::E / R;
+  static_for<0, B>([&](auto bi) {
+    constexpr int b = decltype(bi)::value;
+    const int j = t + b * P::TF;
+    const int base = (j / Ns) * Ns * R + (j & (Ns - 1));
+    const int bp = lpad(base);
+    static_for<0, R>([&](auto ri) {
+      constexpr int r = decltype(ri)::value;
+      lds[lpad_off<r * Ns>(base, bp)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
+    });
+  });
+}
+
+template <class P, int p, int C>
+__device__ __forceinline__ void fft_load_c(float2* v, const float* lds, int t) {
+  constexpr int R = P::R[p];
+  constexpr int B = P::E / R;
+  const int tp = lpad(t);
+  static_for<0, B>([&](auto bi) {
+    constexpr int b = decltype(bi)::value;
+    static_for<0, R>([&](auto ri) {
+      constexpr int r = decltype(ri)::value;
+      const float f = lds[lpad_off<b * P::TF + r * (P::N / R)>(t, tp)];
+      if constexpr (C == 0) v[b * R + r].x = f; else v[b * R + r].y = f;
+    });
+  });
+}
+
+template <class P, int p, class TW>
+__device__ __forceinline__ void fft_tail_split(float2* v, float* lds, TW tws, int t) {
+  if constexpr (p < P::NP) {
+    __syncthreads();
+    fft_store_c<P, p - 1, 0>(v, lds, t);
+    __syncthreads();
+    fft_load_c<P, p, 0>(v, lds, t);
+    __syncthreads();
+    fft_store_c<P, p - 1, 1>(v, lds, t);
+    __syncthreads();
+    fft_load_c<P, p, 1>(v, lds, t);
+    fft_stage<P, p>(v, tws, t);
+    fft_tail_split<P, p + 1>(v, lds, tws, t);
+  }
+}
+
+// Two-level LDS twiddles + split exchange (LDS: P::LDS floats + the table).
+template <class P>
+__device__ __forceinline__ void fft_frame_split(float2* v, float* lds, const float2* t2, int t) {
+  static_assert(P::valid(), "invalid FFT plan");
+  fft_stage<P, 0>(v, TwLds{t2}, t);
+  fft_tail_split<P, 1>(v, lds, TwLds{t2}, t);
+}
+
 template <class P, int p, class TW, class H = NoHook>
 __device__ __forceinline__ void fft_tail(float2* v, float2* lds, TW tws, int t, H hook = H{}) {
   if constexpr (p < P::NP) {

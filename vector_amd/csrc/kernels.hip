@@ -14,6 +14,17 @@
 
 namespace vsig {
 
+// Occupancy request (min waves per SIMD) of a kernel variant: the split
+// exchange (variant 4) exists to fit two 16k / four 8k frames per CU, which
+// needs <= 128 VGPRs, so ask the register allocator for 4 waves/SIMD there.
+template <class P, int PERSIST>
+constexpr int min_waves() { return (PERSIST == 4 && P::E <= 16) ? 4 : 1; }
+
+// Overlap-save kernels run one frame per block: TF threads (one wave for the
+// 1024 / 2048-point plans, whose barriers then cost nothing).
+template <class P>
+constexpr int os_threads() { return P::TF; }
+
 // ---------------------------------------------------------------------------
 // Persistent-kernel skeleton shared by the streaming kernels: a block walks
 // units u = blockIdx.x, + gridDim.x, ...; the next unit's samples are loaded
@@ -39,18 +50,44 @@ __device__ __forceinline__ void psd_load(float2* v, const float2* __restrict__ x
 }
 
 template <class P, int PERSIST>
-__global__ __launch_bounds__(block_threads<P>()) void psd_kernel(
+__global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void psd_kernel(
     const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
     const float2* __restrict__ tw) {
   constexpr int BT = block_threads<P>();
   constexpr int FPB = BT / P::TF;
-  __shared__ float2 lds[FPB * P::LDS + (PERSIST == 3 ? tw2_size<P>() : 0)];
+  __shared__ float2 lds[FPB * (PERSIST == 4 ? (P::LDS + 1) / 2 : P::LDS) +
+                       ((PERSIST == 3 || PERSIST == 4) ? tw2_size<P>() : 0)];
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
   const long long units = (nframes + FPB - 1) / FPB;
   long long u = blockIdx.x;
   if (u >= units) return;
+  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
+    constexpr int FL = (P::LDS + 1) / 2;
+    float2* t2 = lds + FPB * FL;
+    load_tw2<P>(t2, tw, threadIdx.x, BT);
+    float2 v[P::E];
+    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = in_index<P>(t, e);
+      const float w = i < nperseg ? win[i] : 0.f;
+      v[e] = make_float2(v[e].x * w, v[e].y * w);
+    }
+    fft_frame_split<P>(v, reinterpret_cast<float*>(lds + fl * FL), t2, t);
+    const long long frame = u * FPB + fl;
+    if (frame < nframes) {
+      float* of = out + frame * P::N;
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = out_index<P>(t, e);
+        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+      }
+    }
+    return;
+  }
   if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
     float2* t2 = lds + FPB * P::LDS;
     load_tw2<P>(t2, tw, threadIdx.x, BT);
@@ -187,6 +224,14 @@ __global__ __launch_bounds__(block_threads<P>()) void spectrum_prep(
   }
 }
 
+// LDS (in float2) of a one-frame block: data (halved by the split exchange)
+// plus the two-level twiddle table for variants 3 and 4.
+template <class P, int PERSIST>
+constexpr int os_lds() {
+  return (PERSIST == 4 ? (P::LDS + 1) / 2 : P::LDS) +
+         ((PERSIST == 3 || PERSIST == 4) ? tw2_size<P>() : 0);
+}
+
 // Pass-0 operands of an overlap-save segment x[s0 .. s0 + N) with zero fill
 // outside [0, n).  The block-uniform base keeps the address in SGPRs; interior
 // segments (the common case) skip the per-element bounds test.
@@ -242,20 +287,33 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 // and inverse-transformed (conj trick), all in LDS / registers.
 // ---------------------------------------------------------------------------
 template <class P, int PERSIST>
-__global__ __launch_bounds__(block_threads<P>()) void fir_os_kernel(
+__global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
     const float2* __restrict__ tw) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  constexpr int BT = block_threads<P>();
+  constexpr int BT = os_threads<P>();
   static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[P::LDS + (PERSIST == 3 ? tw2_size<P>() : 0)];
+  __shared__ float2 lds[os_lds<P, PERSIST>()];
   const int t = threadIdx.x;
   long long b = blockIdx.x;
   if (b >= nblocks) return;  // uniform per block
 
   const int lo = ntaps - 1;
   const long long nloc = n - g0;
+  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
+    float2* t2 = lds + (P::LDS + 1) / 2;
+    float* ldf = reinterpret_cast<float*>(lds);
+    load_tw2<P>(t2, tw, t, BT);
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame_split<P>(v, ldf, t2, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame_split<P>(v, ldf, t2, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  }
   if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
     float2* t2 = lds + P::LDS;
     load_tw2<P>(t2, tw, t, BT);
@@ -362,7 +420,7 @@ template <class P>
 __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, long long hop,
                                                long long nout, float2* __restrict__ c,
                                                int store_mode, PeakPartial* partials, int t) {
-  constexpr int BT = block_threads<P>();
+  constexpr int BT = os_threads<P>();
   const long long ob = b * hop;                         // block's first output
   const long long rem = nout - ob;
   const int lim = rem < hop ? (int)rem : (int)hop;
@@ -386,18 +444,31 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
 }
 
 template <class P, int PERSIST>
-__global__ __launch_bounds__(block_threads<P>()) void xcorr_os_kernel(
+__global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void xcorr_os_kernel(
     const float2* __restrict__ s, long long n, const float2* __restrict__ Ps, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  constexpr int BT = block_threads<P>();
+  constexpr int BT = os_threads<P>();
   static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[P::LDS + (PERSIST == 3 ? tw2_size<P>() : 0)];
+  __shared__ float2 lds[os_lds<P, PERSIST>()];
   const int t = threadIdx.x;
   long long b = blockIdx.x;
   if (b >= nblocks) return;
 
+  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
+    float2* t2 = lds + (P::LDS + 1) / 2;
+    float* ldf = reinterpret_cast<float*>(lds);
+    load_tw2<P>(t2, tw, t, BT);
+    float2 v[P::E];
+    load_segment<P>(v, s, b * hop - off, n, t);
+    fft_frame_split<P>(v, ldf, t2, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+    fft_frame_split<P>(v, ldf, t2, t);
+    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+    return;
+  }
   if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
     float2* t2 = lds + P::LDS;
     load_tw2<P>(t2, tw, t, BT);
@@ -560,7 +631,8 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                       const float2* tw, int variant, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
   VSIG_PLAN_SWITCH(N, {
-    if (variant & 8) launch_psd_t<PL, 3>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    if (variant & 16) launch_psd_t<PL, 4>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    else if (variant & 8) launch_psd_t<PL, 3>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else if (variant & 4) launch_psd_t<PL, 2>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else if (variant & 1) launch_psd_t<PL, 1>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else launch_psd_t<PL, 0>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
@@ -581,8 +653,12 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 // variant bit 0: persistent (prefetch + register anchors); bit 1: the E = 32 /
 // 512-thread plan for M = 16384 instead of E = 16 / 1024 threads.
 using Plan16384w = Plan<16384, 32, 32, 16, 32>;
+using Plan1024s = Plan<1024, 16, 16, 4, 16>;    // one wave per frame
+using Plan2048s = Plan<2048, 32, 8, 32, 8>;     // one wave per frame
 #define VSIG_OS_SWITCH(N, V, ...)                                          \
   switch (N) {                                                              \
+    case 1024: { using PL = Plan1024s; __VA_ARGS__; } break;                \
+    case 2048: { using PL = Plan2048s; __VA_ARGS__; } break;                \
     case 4096: { using PL = Plan4096; __VA_ARGS__; } break;                        \
     case 8192: { using PL = Plan8192; __VA_ARGS__; } break;                        \
     case 16384:                                                             \
@@ -598,8 +674,8 @@ void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, 
                   hipStream_t st) {
   const long long grid =
       (PERSIST == 1 || PERSIST == 2)
-          ? persistent_grid(fir_os_kernel<PL, PERSIST>, block_threads<PL>(), nblocks) : nblocks;
-  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(block_threads<PL>()),
+          ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks) : nblocks;
+  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(os_threads<PL>()),
                      0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
 }
 
@@ -609,7 +685,8 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
   VSIG_OS_SWITCH(M, variant, {
-    if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    if (variant & 16) launch_fir_t<PL, 4>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 4) launch_fir_t<PL, 2>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else launch_fir_t<PL, 0>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
@@ -623,9 +700,9 @@ void launch_xcorr_t(const float2* s, long long n, const float2* Ps, long long of
                     long long nblocks, const float2* tw, hipStream_t st) {
   const long long grid =
       (PERSIST == 1 || PERSIST == 2)
-          ? persistent_grid(xcorr_os_kernel<PL, PERSIST>, block_threads<PL>(), nblocks) : nblocks;
+          ? persistent_grid(xcorr_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks) : nblocks;
   hipLaunchKernelGGL((xcorr_os_kernel<PL, PERSIST>), dim3((unsigned)grid),
-                     dim3(block_threads<PL>()), 0, st, s, n, Ps, off, nout, hop, c, store_mode,
+                     dim3(os_threads<PL>()), 0, st, s, n, Ps, off, nout, hop, c, store_mode,
                      partials, nblocks, tw);
 }
 
@@ -635,7 +712,8 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
   VSIG_OS_SWITCH(M, variant, {
-    if (variant & 8) launch_xcorr_t<PL, 3>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+    if (variant & 16) launch_xcorr_t<PL, 4>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+    else if (variant & 8) launch_xcorr_t<PL, 3>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
     else if (variant & 4) launch_xcorr_t<PL, 2>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
     else if (variant & 1) launch_xcorr_t<PL, 1>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
     else launch_xcorr_t<PL, 0>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
@@ -666,6 +744,8 @@ hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, i
 namespace vsig {
 hipError_t tw2_info(int N, int* shift, int* hi) {
   if (N == -16384) { *shift = tw2_shift<Plan16384w>(); *hi = tw2_hi<Plan16384w>(); return hipSuccess; }
+  if (N == -1024) { *shift = tw2_shift<Plan1024s>(); *hi = tw2_hi<Plan1024s>(); return hipSuccess; }
+  if (N == -2048) { *shift = tw2_shift<Plan2048s>(); *hi = tw2_hi<Plan2048s>(); return hipSuccess; }
   VSIG_PLAN_SWITCH(N, { *shift = tw2_shift<PL>(); *hi = tw2_hi<PL>(); });
   return hipSuccess;
 }
@@ -674,6 +754,12 @@ hipError_t plan_info(int N, int* radices, int* npasses) {
   if (N == -16384) {   // the E = 32 plan of 16384 points (variant bit 1)
     *npasses = Plan16384w::NP;
     for (int q = 0; q < Plan16384w::NP; ++q) radices[q] = Plan16384w::R[q];
+    return hipSuccess;
+  }
+  if (N == -1024 || N == -2048) {   // one-wave overlap-save plans
+    const int np = N == -1024 ? Plan1024s::NP : Plan2048s::NP;
+    *npasses = np;
+    for (int q = 0; q < np; ++q) radices[q] = N == -1024 ? Plan1024s::R[q] : Plan2048s::R[q];
     return hipSuccess;
   }
   VSIG_PLAN_SWITCH(N, {

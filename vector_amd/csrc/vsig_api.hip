@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{8, 8, 10};         // tuned defaults (see vsig_set_option)
+  vsig::Variants var{16, 8, 10};         // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
 };
 
@@ -90,7 +90,11 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
   return VSIG_OK;
 }
 
-int tw_key(int M, int variant) { return (M == 16384 && (variant & 2)) ? -16384 : M; }
+// Twiddle-table key of the plan an overlap-save launch of size M uses.
+int tw_key(int M, int variant) {
+  if (M == 1024 || M == 2048) return -M;           // one-wave plans
+  return (M == 16384 && (variant & 2)) ? -16384 : M;
+}
 
 // Two-level table for plan key N (cached under key N + 2^20).
 int get_tw2(vsig_ctx* c, int N, const float2** out) {
@@ -118,10 +122,11 @@ int get_tw2(vsig_ctx* c, int N, const float2** out) {
   return VSIG_OK;
 }
 
-// Twiddle operand of a launch: the per-pass table, or (variant bit 3) the
-// two-level table.
-int get_tw_for(vsig_ctx* c, int M, int variant, const float2** out) {
-  return (variant & 8) ? get_tw2(c, tw_key(M, variant), out) : get_twiddles(c, tw_key(M, variant), out);
+// Twiddle operand of a launch: the per-pass table, or (variant bits 3/4) the
+// two-level table.  os: an overlap-save launch (its own plans for 1k / 2k / 16k).
+int get_tw_for(vsig_ctx* c, int M, int variant, bool os, const float2** out) {
+  const int key = os ? tw_key(M, variant) : M;
+  return (variant & 24) ? get_tw2(c, key, out) : get_twiddles(c, key, out);
 }
 
 int ensure_partials(vsig_ctx* c, long long n) {
@@ -171,11 +176,13 @@ int env_size(const char* name, int dflt, int minlen) {
   const char* e = getenv(name);
   if (!e) return dflt;
   const int v = atoi(e);
-  if ((v == 4096 || v == 8192 || v == 16384) && v >= 2 * minlen) return v;
+  if ((v == 1024 || v == 2048 || v == 4096 || v == 8192 || v == 16384) && v >= 2 * minlen)
+    return v;
   return dflt;
 }
 
 int os_size_fir_default(int ntaps) {
+  if (ntaps <= 256) return 1024;      // one-wave blocks; hop >= 769 (measured best at 255 taps)
   if (ntaps <= 512) return 4096;
   if (ntaps <= 2048) return 8192;
   if (ntaps <= 8192) return 16384;
@@ -226,7 +233,7 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, int L, const float2* s, long
   int rc = ensure_partials(c, nblocks);
   if (rc) return rc;
   const float2* tw;
-  rc = get_tw_for(c, M, c->var.xcorr, &tw);
+  rc = get_tw_for(c, M, c->var.xcorr, true, &tw);
   if (rc) return rc;
   {
     Timed t(c, "xcorr");
@@ -305,12 +312,13 @@ int vsig_set_stream(vsig_ctx* c, void* s) {
 int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   if (!c || !key) return VSIG_E_INVALID;
   const std::string k(key);
-  if (k == "psd_variant") c->var.psd = value & 13;
-  else if (k == "fir_variant") c->var.fir = value & 15;
-  else if (k == "xcorr_variant") c->var.xcorr = value & 15;
+  if (k == "psd_variant") c->var.psd = value & 29;
+  else if (k == "fir_variant") c->var.fir = value & 31;
+  else if (k == "xcorr_variant") c->var.xcorr = value & 31;
   else if (k == "fir_m" || k == "xcorr_m") {
-    if (value != 0 && value != 4096 && value != 8192 && value != 16384)
-      return fail(c, VSIG_E_INVALID, "block size must be 0, 4096, 8192 or 16384");
+    if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
+        value != 16384)
+      return fail(c, VSIG_E_INVALID, "block size must be 0, 1024, 2048, 4096, 8192 or 16384");
     (k == "fir_m" ? c->fir_m : c->xcorr_m) = value;
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
@@ -358,7 +366,7 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
     return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
   const float2* tw;
-  int rc = get_tw_for(c, nfft, c->var.psd & 8, &tw);
+  int rc = get_tw_for(c, nfft, c->var.psd, false, &tw);
   if (rc) return rc;
   Timed t(c, "psd");
   HIPCHK(c, vsig::launch_psd(nfft, (const float2*)x, stride, win, nperseg, hop, scale, sxx, nframes,
@@ -422,7 +430,7 @@ int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n,
   if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
-  int rc = get_tw_for(c, f->M, c->var.fir, &tw);
+  int rc = get_tw_for(c, f->M, c->var.fir, true, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,
