@@ -85,6 +85,10 @@ int vsig_synchronize(vsig_ctx* ctx);
  *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule.
  * Plans created afterwards use the new block sizes. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
+/* Tuning micro-benchmark: `iters` in-LDS FFTs on each of `frames` frames of
+ * the plan `key` (4096 / 8192 / 16384, -1024 / -2048 / -16384 for the
+ * overlap-save one-wave and 512-thread plans); io: frames * |key| complex64. */
+int vsig_fft_bench(vsig_ctx* ctx, int key, void* io, int frames, int iters, int twl);
 /* Per-kernel timing with HIP events on the context stream (for bench.py):
  * enable, run, then read the mean duration in ms of each kernel family. */
 int vsig_timing_enable(vsig_ctx* ctx, int on);

@@ -267,7 +267,7 @@ def test_correlator_stream_full_size_property(gpu):
     assert peak == pytest.approx(direct, rel=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40])
 def test_kernel_variants_agree_with_oracle(gpu, variant):
     """Every tuning variant (persistent / LDS twiddles / split exchange /
     512-thread 16k plan) must give the same results as the oracle."""
@@ -293,6 +293,22 @@ def test_kernel_variants_agree_with_oracle(gpu, variant):
             c, _ = gpu.cross_correlate_signals(tmpl, x, "valid")
             r, _ = ref.cross_correlate_signals(tmpl, x, "valid")
             assert_normwise(c, r, XC_TOL)
+        # streaming Correlator (partitioned when variant bit 5), valid and full
+        import torch
+        s = torch.from_numpy(x).cuda()
+        for L in (4096, 3000, 1500):
+            xc = gpu.Correlator(tmpl[:L])
+            for mode in ("valid", "full"):
+                nout = len(x) - L + 1 if mode == "valid" else len(x) + L - 1
+                out = torch.empty(nout, dtype=torch.complex64, device="cuda")
+                _, pk = xc(s, mode, out=out)
+                r, _ = ref.cross_correlate_signals(tmpl[:L], x, mode)
+                assert_normwise(out.cpu().numpy(), r, XC_TOL)
+                peak, idx, s1, s2 = gpu.dsp._read_peak(pk)
+                a = np.abs(r)
+                assert idx == int(np.argmax(a))
+                assert peak == pytest.approx(a.max(), rel=1e-5)
+                assert s1 == pytest.approx(a.sum(), rel=1e-5)
     finally:
         lib, h = ctx.lib, ctx.h
         lib.vsig_set_option(h, b"psd_variant", 8)

@@ -460,6 +460,10 @@ using Plan2048 = Plan<2048, 32, 8, 32, 8>;
 using Plan4096 = Plan<4096, 16, 16, 16, 16>;
 using Plan8192 = Plan<8192, 32, 16, 32, 16>;
 using Plan16384 = Plan<16384, 16, 16, 4, 16, 16>;
+// Overlap-save alternatives: 512-thread 16k plan; one-wave 1k / 2k plans.
+using Plan16384w = Plan<16384, 32, 32, 16, 32>;
+using Plan1024s = Plan<1024, 16, 16, 4, 16>;
+using Plan2048s = Plan<2048, 32, 8, 32, 8>;
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

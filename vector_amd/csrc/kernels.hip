@@ -527,6 +527,104 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void xc
 }
 
 // ---------------------------------------------------------------------------
+// Partitioned cross-correlation (uniformly partitioned overlap-save): the
+// template is cut into two halves of Lp = M/2 samples; hop j's outputs are
+//   c[j*Lp + i] = IFFT( X_j conj(P0) + X_{j+1} conj(P1) )[i],   i < Lp,
+// X_j = FFT_M(s[j*Lp - off ...]).  A block walks a contiguous run of hops,
+// carrying X_{j+1} in registers into hop j+1, so each hop costs one forward and
+// one inverse M-point FFT: M = L-point FFTs (4 blocks / CU at L = 4096) instead
+// of the 4L-point FFTs plain overlap-save needs for the same efficiency.
+// ---------------------------------------------------------------------------
+template <class P, int TWL>
+__global__ __launch_bounds__(os_threads<P>(), 3) void xcorr_part_kernel(
+    const float2* __restrict__ s, long long n, const float2* __restrict__ P0,
+    const float2* __restrict__ P1, long long off, long long nout, int Lp, long long nhops,
+    long long hpb, float2* __restrict__ c, int store_mode, PeakPartial* __restrict__ partials,
+    const float2* __restrict__ tw) {
+  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+  constexpr int BT = os_threads<P>();
+  __shared__ float2 lds[P::LDS + (TWL ? tw2_size<P>() : 0)];
+  const int t = threadIdx.x;
+  const long long j0 = (long long)blockIdx.x * hpb;
+  const long long j1 = j0 + hpb < nhops ? j0 + hpb : nhops;
+  if (j0 >= j1) return;
+  float2* t2 = lds + P::LDS;
+  if constexpr (TWL) load_tw2<P>(t2, tw, t, BT);
+  auto fft = [&](float2* v, int tt) {
+    if constexpr (TWL) fft_frame_t2<P>(v, lds, t2, tt);
+    else fft_frame<P>(v, lds, tw, tt);
+  };
+  float2 xn[P::E];                      // X_{j+1} of the previous hop
+  load_segment<P>(xn, s, j0 * Lp - off, n, t);
+  fft(xn, t);
+  for (long long j = j0; j < j1; ++j) {
+    // An opaque copy of the thread index: keeps the (loop-invariant) LDS and
+    // twiddle address arithmetic of the three FFTs inside the loop instead of
+    // hoisted into hundreds of live VGPRs.
+    const int tt = t + opaque_zero();
+    float2 v[P::E];
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(xn[e]), P0[out_index<P>(tt, e)]);
+    load_segment<P>(xn, s, (j + 1) * Lp - off, n, tt);
+    fft(xn, tt);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const float2 a = cmul(cconj(xn[e]), P1[out_index<P>(tt, e)]);
+      v[e] = cadd(v[e], a);
+    }
+    fft(v, tt);
+    xcorr_epilogue<P>(v, j, Lp, nout, c, store_mode, partials, tt);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Engine micro-benchmark (tuning only): `iters` back-to-back FFTs of one frame
+// per block with no HBM traffic in the loop — the compute/LDS ceiling of a plan.
+// ---------------------------------------------------------------------------
+template <class P, int TWL>
+__global__ __launch_bounds__(os_threads<P>()) void fft_bench_kernel(float2* __restrict__ io,
+                                                                    int iters,
+                                                                    const float2* __restrict__ tw) {
+  __shared__ float2 lds[P::LDS + (TWL ? tw2_size<P>() : 0)];
+  const int t = threadIdx.x;
+  float2* t2 = lds + P::LDS;
+  if constexpr (TWL) load_tw2<P>(t2, tw, t, os_threads<P>());
+  float2 v[P::E];
+  float2* f = io + (long long)blockIdx.x * P::N;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) v[e] = f[in_index<P>(t, e)];
+  for (int it = 0; it < iters; ++it) {
+    const int tt = t + opaque_zero();
+    if constexpr (TWL) fft_frame_t2<P>(v, lds, t2, tt);
+    else fft_frame<P>(v, lds, tw, tt);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = make_float2(v[e].x * 1e-4f, v[e].y * 1e-4f);
+  }
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) f[out_index<P>(t, e)] = v[e];
+}
+
+hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const float2* tw, int twl,
+                            hipStream_t st) {
+#define VSIG_FB(PL)                                                                          \
+  {                                                                                          \
+    auto k = twl ? fft_bench_kernel<PL, 1> : fft_bench_kernel<PL, 0>;                         \
+    hipLaunchKernelGGL(k, dim3(frames), dim3(os_threads<PL>()), 0, st, io, iters, tw);        \
+  }
+  switch (key) {
+    case -1024: VSIG_FB(Plan1024s) break;
+    case -2048: VSIG_FB(Plan2048s) break;
+    case 4096: VSIG_FB(Plan4096) break;
+    case 8192: VSIG_FB(Plan8192) break;
+    case 16384: VSIG_FB(Plan16384) break;
+    case -16384: VSIG_FB(Plan16384w) break;
+    default: return hipErrorInvalidValue;
+  }
+#undef VSIG_FB
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // |c| reduction over an array in double precision (find_correlation_peak,
 // utils.py:1321-1334): |c| = hypot(re, im) like np.abs, first max wins.
 // T = double2 (complex128), float2 (complex64), double, float.
@@ -652,9 +750,6 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 // Only plans with one frame per block can run the overlap-save kernels.
 // variant bit 0: persistent (prefetch + register anchors); bit 1: the E = 32 /
 // 512-thread plan for M = 16384 instead of E = 16 / 1024 threads.
-using Plan16384w = Plan<16384, 32, 32, 16, 32>;
-using Plan1024s = Plan<1024, 16, 16, 4, 16>;    // one wave per frame
-using Plan2048s = Plan<2048, 32, 8, 32, 8>;     // one wave per frame
 #define VSIG_OS_SWITCH(N, V, ...)                                          \
   switch (N) {                                                              \
     case 1024: { using PL = Plan1024s; __VA_ARGS__; } break;                \
@@ -717,6 +812,24 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
     else if (variant & 4) launch_xcorr_t<PL, 2>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
     else if (variant & 1) launch_xcorr_t<PL, 1>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
     else launch_xcorr_t<PL, 0>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
+  });
+  return hipGetLastError();
+}
+
+hipError_t launch_xcorr_part(int M, const float2* s, long long n, const float2* P0,
+                             const float2* P1, long long off, long long nout, float2* c,
+                             int store_mode, PeakPartial* partials, const float2* tw, int twl,
+                             hipStream_t st) {
+  if (nout <= 0) return hipSuccess;
+  const int Lp = M / 2;
+  const long long nhops = (nout + Lp - 1) / Lp;
+  VSIG_OS_SWITCH(M, 0, {
+    auto k = twl ? xcorr_part_kernel<PL, 1> : xcorr_part_kernel<PL, 0>;
+    const long long g = persistent_grid(k, os_threads<PL>(), nhops);
+    const long long hpb = (nhops + g - 1) / g;
+    const long long grid = (nhops + hpb - 1) / hpb;
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(os_threads<PL>()), 0, st, s, n, P0, P1,
+                       off, nout, Lp, nhops, hpb, c, store_mode, partials, tw);
   });
   return hipGetLastError();
 }

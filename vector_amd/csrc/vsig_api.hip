@@ -45,6 +45,7 @@ struct vsig_xcorr {
   vsig_ctx* ctx;
   int L, M;
   float2* Ps;
+  float2* Ps1;   // partitioned mode: spectrum of the template's second half (else null)
 };
 
 namespace {
@@ -224,21 +225,28 @@ int finalize_peak(vsig_ctx* c, long long nparts, int sqrt_max, vsig_peak_t* peak
   return VSIG_OK;
 }
 
-// Shared by the plan-based and the general correlation paths.
-int run_xcorr(vsig_ctx* c, int M, const float2* Ps, int L, const float2* s, long long n,
-              long long off, long long nout, int store_mode, void* cout, vsig_peak_t* peak_dev) {
-  const long long hop = (long long)M - L + 1;
-  const long long nblocks = nout > 0 ? (nout + hop - 1) / hop : 0;
+// Shared by the plan-based and the general correlation paths.  Ps1 != null:
+// partitioned correlation (template halves of M/2, see xcorr_part_kernel).
+int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, const float2* s,
+              long long n, long long off, long long nout, int store_mode, void* cout,
+              vsig_peak_t* peak_dev) {
   if (nout <= 0) return fail(c, VSIG_E_INVALID, "empty correlation output");
+  const long long hop = Ps1 ? (long long)M / 2 : (long long)M - L + 1;
+  const long long nblocks = (nout + hop - 1) / hop;
   int rc = ensure_partials(c, nblocks);
   if (rc) return rc;
   const float2* tw;
-  rc = get_tw_for(c, M, c->var.xcorr, true, &tw);
+  const int var = Ps1 ? (c->var.xcorr & 8) : c->var.xcorr;
+  rc = get_tw_for(c, M, var, true, &tw);
   if (rc) return rc;
   {
     Timed t(c, "xcorr");
-    HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
-                                    c->partials, tw, c->var.xcorr, c->stream));
+    if (Ps1)
+      HIPCHK(c, vsig::launch_xcorr_part(M, s, n, Ps, Ps1, off, nout, (float2*)cout, store_mode,
+                                        c->partials, tw, (var & 8) ? 1 : 0, c->stream));
+    else
+      HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
+                                      c->partials, tw, c->var.xcorr, c->stream));
   }
   return finalize_peak(c, nblocks, 1, peak_dev);
 }
@@ -314,7 +322,7 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   const std::string k(key);
   if (k == "psd_variant") c->var.psd = value & 29;
   else if (k == "fir_variant") c->var.fir = value & 31;
-  else if (k == "xcorr_variant") c->var.xcorr = value & 31;
+  else if (k == "xcorr_variant") c->var.xcorr = value & 63;
   else if (k == "fir_m" || k == "xcorr_m") {
     if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
         value != 16384)
@@ -323,6 +331,16 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }
+  return VSIG_OK;
+}
+
+int vsig_fft_bench(vsig_ctx* c, int key, void* io, int frames, int iters, int twl) {
+  if (!c || !io || frames < 1 || iters < 1) return fail(c, VSIG_E_INVALID, "bad arguments");
+  const float2* tw;
+  int rc = twl ? get_tw2(c, key, &tw) : get_twiddles(c, key, &tw);
+  if (rc) return rc;
+  Timed t(c, "fft_bench");
+  HIPCHK(c, vsig::launch_fft_bench(key, (float2*)io, frames, iters, tw, twl, c->stream));
   return VSIG_OK;
 }
 
@@ -470,18 +488,31 @@ int vsig_xcorr_create(vsig_ctx* c, const void* tmpl, int32_t L, vsig_xcorr** out
   if (!c || !tmpl || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   *out = nullptr;
   if (L < 1) return fail(c, VSIG_E_INVALID, "template length must be >= 1");
-  const int M = os_size_xcorr(c, L);
+  // Partitioned mode (variant bit 5): M = next power of two >= L, halves of M/2.
+  int Mp = 2048;
+  while (Mp < L) Mp *= 2;
+  const bool part = (c->var.xcorr & 32) && L > 1024 && Mp <= 16384;
+  const int M = part ? Mp : os_size_xcorr(c, L);
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "template longer than 8192");
   float2* td = nullptr;
   HIPCHK(c, hipMalloc(&td, (size_t)L * sizeof(float2)));
   hipError_t e = hipMemcpyAsync(td, tmpl, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, c->stream);
   if (e != hipSuccess) { (void)hipFree(td); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
-  float2* Ps = nullptr;
-  int rc = make_spectrum(c, td, L, M, &Ps);
+  float2 *Ps = nullptr, *Ps1 = nullptr;
+  int rc;
+  if (part) {
+    rc = make_spectrum(c, td, M / 2, M, &Ps);
+    if (!rc) rc = make_spectrum(c, td + M / 2, L - M / 2, M, &Ps1);
+  } else {
+    rc = make_spectrum(c, td, L, M, &Ps);
+  }
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(td);
-  if (rc) return rc;
-  *out = new vsig_xcorr{c, L, M, Ps};
+  if (rc) {
+    if (Ps) (void)hipFree(Ps);
+    return rc;
+  }
+  *out = new vsig_xcorr{c, L, M, Ps, Ps1};
   return VSIG_OK;
 }
 
@@ -489,6 +520,7 @@ void vsig_xcorr_free(vsig_xcorr* x) {
   if (!x) return;
   (void)hipStreamSynchronize(x->ctx->stream);
   (void)hipFree(x->Ps);
+  if (x->Ps1) (void)hipFree(x->Ps1);
   delete x;
 }
 
@@ -502,8 +534,8 @@ int vsig_xcorr_exec_dev(vsig_xcorr* x, const void* s, int64_t n, int32_t mode, v
   else if (mode == VSIG_MODE_FULL) { off = x->L - 1; nout = n + x->L - 1; }
   else return fail(c, VSIG_E_INVALID, "streaming correlation supports VALID and FULL");
   if (nout < 1) return fail(c, VSIG_E_INVALID, "stream shorter than the template");
-  return run_xcorr(c, x->M, x->Ps, x->L, (const float2*)s, n, off, nout, cout ? 1 : 0, cout,
-                   peak_dev);
+  return run_xcorr(c, x->M, x->Ps, x->Ps1, x->L, (const float2*)s, n, off, nout, cout ? 1 : 0,
+                   cout, peak_dev);
 }
 
 int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
@@ -529,7 +561,8 @@ int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v
   // Not swapped: kernel offset off = (L-1) - F.  Swapped: compute the
   // correlation of v by a and store conj() reversed, off' = F + nout - nv.
   const long long off = swap ? F + nout - nv : (L - 1) - F;
-  rc = run_xcorr(c, M, Ps, L, strm, nmax, off, nout, cout ? (swap ? 2 : 1) : 0, cout, peak_dev);
+  rc = run_xcorr(c, M, Ps, nullptr, L, strm, nmax, off, nout, cout ? (swap ? 2 : 1) : 0, cout,
+                 peak_dev);
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(Ps);
   return rc;

@@ -22,7 +22,8 @@ hipError_t tw2_info(int N, int* shift, int* hi);
 
 // Kernel variants (tuning): bit 0 persistent + register twiddle anchors;
 // bit 1 (M = 16384) E = 32 plan; bit 2 persistent + late prefetch; bit 3
-// two-level LDS twiddle table (one unit per block).
+// two-level LDS twiddle table (one unit per block); bit 4 split re/im LDS
+// exchange; bit 5 (xcorr) partitioned correlation with M = L-point FFTs.
 struct Variants { int psd, fir, xcorr; };
 
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
@@ -37,6 +38,14 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, int variant,
                            hipStream_t st);
+// Partitioned correlation (template halves P0 / P1 of Lp = M / 2 samples).
+hipError_t launch_xcorr_part(int M, const float2* s, long long n, const float2* P0,
+                             const float2* P1, long long off, long long nout, float2* c,
+                             int store_mode, PeakPartial* partials, const float2* tw, int twl,
+                             hipStream_t st);
+// Tuning micro-benchmark: iters FFTs per frame, frames blocks (key: plan key).
+hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const float2* tw, int twl,
+                            hipStream_t st);
 hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
                               int nparts, hipStream_t st);
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
