@@ -145,6 +145,25 @@ int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, 
 int vsig_peak_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev);
 int vsig_peak(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak);
 
+/* ---- analysis (normalize_spectrogram utils.py:356-404, find_packet_start /
+ * detect_packet_bounds utils.py:784-825).  All operate on |a|.
+ * vsig_select_dev: k-th smallest |a| for up to 4 0-based ranks (host output;
+ *   np.percentile / np.median are interpolations of these).
+ * vsig_threshold_dev: count / first / last index of |a| >= thr and max |a|.
+ * vsig_boxcar_energy_dev: sm = np.convolve(np.abs(x)**2, ones(w)/w, 'same')
+ *   in double (x of any VSIG_DTYPE; sm: max(n, w) doubles on the device).
+ * vsig_db_dev: out = 10 log10(|a| + floor), F32 -> float32 math and output,
+ *   F64 -> double (numpy's promotion in normalize_spectrogram).
+ * vsig_abs_c64_dev: out = |a| + 0j as complex64 (a of any VSIG_DTYPE). */
+int vsig_select_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, const int64_t* ranks,
+                    int32_t nranks, double* values);
+int vsig_threshold_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, double thr,
+                       int64_t* count, int64_t* first, int64_t* last, double* maxval);
+int vsig_boxcar_energy_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t n, int64_t w,
+                           double* sm);
+int vsig_db_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, double floor_, void* out);
+int vsig_abs_c64_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, void* out);
+
 #ifdef __cplusplus
 }
 #endif

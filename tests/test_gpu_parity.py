@@ -212,6 +212,26 @@ def test_correlate_swapped_lengths_and_small(gpu):
             assert_normwise(c, r, XC_TOL)
 
 
+def test_correlate_peak_swapped_operands(gpu):
+    """signal2 shorter than signal1: np.correlate swaps its operands and
+    reverses the output; the fused argmax must index the reversed output
+    (ties are broken toward the first reversed index, but the fp32 FFT's
+    rounding means flat |c| runs are not exact ties, so none are asserted)."""
+    rng = np.random.default_rng(12)
+    for l1, l2 in ((300, 40), (5000, 700), (9000, 8192)):
+        s1 = (rng.standard_normal(l1) + 1j * rng.standard_normal(l1)).astype(np.complex64)
+        s2 = s1[l1 // 3:l1 // 3 + l2].copy()
+        lag, val, _ = gpu.correlate_peak(s1, s2, "full")
+        r_i, r_lag, r_peak, *_ = ref.xcorr_peak(s2, s1, "full")   # (stream, preamble)
+        assert lag == r_lag, (l1, l2, lag, r_lag)
+        assert val == pytest.approx(r_peak, rel=1e-5)
+        # 'valid' with signal2 shorter: the reference's lag axis is empty
+        with pytest.raises(IndexError):
+            ref.xcorr_peak(s2, s1, "valid")
+        with pytest.raises(IndexError):
+            gpu.correlate_peak(s1, s2, "valid")
+
+
 def test_correlate_peak_4096_preamble(gpu):
     g = golden("xcorr_peak.npz")
     lag, val, conf = gpu.correlate_peak(g["pre"], g["x"], "valid")

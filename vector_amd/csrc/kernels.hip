@@ -412,8 +412,10 @@ __device__ __forceinline__ void block_partial(double m, long long mi, double s1,
 // Cross-correlation, overlap-save:  c[o] = sum_{k<L} s[o - off + k] * conj(p[k]),
 // o in [0, nout).  off = 0 -> np.correlate 'valid'; off = L-1 -> 'full'.
 // Block b: outputs [b*hop, b*hop + hop), hop <= M - L + 1.
-// Epilogue: optional store of c (or of conj(c) at nout-1-o, for the swapped
-// argument order of np.correlate), and the block's |c| partial.
+// Epilogue: optional store of c (store_mode 1) or of conj(c) at nout-1-o
+// (store_mode 2, the swapped argument order of np.correlate), and the block's
+// |c| partial; store_mode bit 4 reports the argmax in the reversed index
+// space (first maximum of the reversed output).
 // ---------------------------------------------------------------------------
 // Epilogue of one correlation block: |c|^2, block argmax / sums, optional store.
 template <class P>
@@ -424,8 +426,10 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
   const long long ob = b * hop;                         // block's first output
   const long long rem = nout - ob;
   const int lim = rem < hop ? (int)rem : (int)hop;
+  const bool rev = store_mode & 4;
+  const int smode = store_mode & 3;
   float m = -1.f;
-  int mi = 0x7fffffff;
+  int mi = rev ? -1 : 0x7fffffff;
   float s1 = 0.f, s2 = 0.f;
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
@@ -433,14 +437,18 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
     if (i < lim) {
       const float2 cv = cconj(v[e]);
       const float a2 = cv.x * cv.x + cv.y * cv.y;
-      if (a2 > m || (a2 == m && i < mi)) { m = a2; mi = i; }
+      if (a2 > m || (a2 == m && (rev ? i > mi : i < mi))) { m = a2; mi = i; }
       s1 += sqrtf(a2);
       s2 += a2;
-      if (store_mode == 1) (c + ob)[(unsigned)i] = cv;
-      else if (store_mode == 2) (c + (nout - 1 - ob))[-i] = cconj(cv);
+      if (smode == 1) (c + ob)[(unsigned)i] = cv;
+      else if (smode == 2) (c + (nout - 1 - ob))[-i] = cconj(cv);
     }
   }
-  if (partials) block_partial<BT>((double)m, ob + mi, (double)s1, (double)s2, partials + b);
+  if (partials) {
+    long long gi = ob + mi;
+    if (rev) gi = m < 0.f ? 0x7fffffffffffffffll : nout - 1 - gi;
+    block_partial<BT>((double)m, gi, (double)s1, (double)s2, partials + b);
+  }
 }
 
 template <class P, int PERSIST>

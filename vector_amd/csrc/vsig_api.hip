@@ -561,7 +561,8 @@ int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v
   // Not swapped: kernel offset off = (L-1) - F.  Swapped: compute the
   // correlation of v by a and store conj() reversed, off' = F + nout - nv.
   const long long off = swap ? F + nout - nv : (L - 1) - F;
-  rc = run_xcorr(c, M, Ps, nullptr, L, strm, nmax, off, nout, cout ? (swap ? 2 : 1) : 0, cout,
+  rc = run_xcorr(c, M, Ps, nullptr, L, strm, nmax, off, nout,
+                 (cout ? (swap ? 2 : 1) : 0) | (swap ? 4 : 0), cout,
                  peak_dev);
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(Ps);
@@ -617,6 +618,121 @@ int vsig_peak(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, vsig_peak_t*
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(peak, c->result, sizeof(vsig_peak_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+// ---------------------------------------------------------------- analysis
+// k-th smallest of |a| (0-based ranks) by MSB-first 8-bit radix select:
+// ceil(bits/8) histogram passes over the data, all ranks at once.
+int vsig_select_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, const int64_t* ranks,
+                    int32_t nranks, double* values) {
+  if (!c || !a || !ranks || !values) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (dtype != VSIG_DTYPE_F32 && dtype != VSIG_DTYPE_F64) return fail(c, VSIG_E_INVALID, "dtype");
+  if (nranks < 1 || nranks > 4 || n < 1) return fail(c, VSIG_E_INVALID, "1..4 ranks, n >= 1");
+  for (int q = 0; q < nranks; ++q)
+    if (ranks[q] < 0 || ranks[q] >= n) return fail(c, VSIG_E_INVALID, "rank out of range");
+  const int bits = dtype == VSIG_DTYPE_F32 ? 32 : 64;
+  unsigned long long pf[4] = {0, 0, 0, 0}, mk[4] = {0, 0, 0, 0};
+  long long k[4];
+  for (int q = 0; q < nranks; ++q) k[q] = ranks[q];
+  int rc = ensure_stage(c, 2, 4096 * 8 + 64);
+  if (rc) return rc;
+  unsigned long long* dhist = (unsigned long long*)c->stage[2];
+  unsigned long long* dpf = dhist + 4 * 256;
+  unsigned long long* dmk = dpf + 4;
+  std::vector<unsigned long long> h(4 * 256);
+  for (int shift = bits - 8; shift >= 0; shift -= 8) {
+    HIPCHK(c, hipMemsetAsync(dhist, 0, 4 * 256 * 8, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dpf, pf, sizeof(pf), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, hipMemcpyAsync(dmk, mk, sizeof(mk), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(c, vsig::launch_radix_hist(dtype, a, n, dpf, dmk, nranks, shift, dhist, c->stream));
+    HIPCHK(c, hipMemcpyAsync(h.data(), dhist, 4 * 256 * 8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (int q = 0; q < nranks; ++q) {
+      long long acc = 0;
+      int d = 0;
+      for (; d < 255; ++d) {
+        const long long cnt = (long long)h[q * 256 + d];
+        if (k[q] < acc + cnt) break;
+        acc += cnt;
+      }
+      k[q] -= acc;
+      pf[q] |= (unsigned long long)d << shift;
+      mk[q] |= 0xffull << shift;
+    }
+  }
+  for (int q = 0; q < nranks; ++q) {
+    // invert the order-preserving key (|a| >= 0: sign bit set, no flip)
+    if (bits == 32) {
+      const unsigned int u = (unsigned int)pf[q] & 0x7fffffffu;
+      float f;
+      memcpy(&f, &u, 4);
+      values[q] = (double)f;
+    } else {
+      const unsigned long long u = pf[q] & 0x7fffffffffffffffull;
+      double d;
+      memcpy(&d, &u, 8);
+      values[q] = d;
+    }
+  }
+  return VSIG_OK;
+}
+
+int vsig_threshold_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, double thr,
+                       int64_t* count, int64_t* first, int64_t* last, double* maxval) {
+  if (!c || !a || !count || !first || !last || !maxval) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (dtype != VSIG_DTYPE_F32 && dtype != VSIG_DTYPE_F64) return fail(c, VSIG_E_INVALID, "dtype");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  long long nparts = (n + 255) / 256;
+  if (nparts > 2048) nparts = 2048;
+  int rc = ensure_stage(c, 2, (size_t)nparts * sizeof(vsig::ThreshPartialH));
+  if (rc) return rc;
+  HIPCHK(c, vsig::launch_thresh_reduce(dtype, a, n, thr, c->stage[2], (int)nparts, c->stream));
+  std::vector<vsig::ThreshPartialH> h(nparts);
+  HIPCHK(c, hipMemcpyAsync(h.data(), c->stage[2], nparts * sizeof(vsig::ThreshPartialH),
+                           hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  long long cnt = 0, f = n, l = -1;
+  double mx = -INFINITY;
+  for (auto& p : h) {
+    cnt += p.count;
+    f = p.first < f ? p.first : f;
+    l = p.last > l ? p.last : l;
+    mx = p.max > mx ? p.max : mx;
+  }
+  *count = cnt;
+  *first = f;
+  *last = l;
+  *maxval = mx;
+  return VSIG_OK;
+}
+
+int vsig_boxcar_energy_dev(vsig_ctx* c, int32_t dtype, const void* x, int64_t n, int64_t w,
+                           double* sm) {
+  if (!c || !x || !sm) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (dtype < VSIG_DTYPE_C128 || dtype > VSIG_DTYPE_F32) return fail(c, VSIG_E_INVALID, "dtype");
+  if (n < 1 || w < 1) return fail(c, VSIG_E_INVALID, "need n >= 1, w >= 1");
+  const long long nt = vsig::energy_scan_tiles(n);
+  int rc;
+  if ((rc = ensure_stage(c, 1, (size_t)nt * 8)) || (rc = ensure_stage(c, 2, (size_t)n * 8))) return rc;
+  double* P = (double*)c->stage[2];
+  HIPCHK(c, vsig::launch_energy_prefix(dtype, x, n, (double*)c->stage[1], P, c->stream));
+  HIPCHK(c, vsig::launch_boxcar_same(P, n, w, sm, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));   // stage buffers are reused by the next call
+  return VSIG_OK;
+}
+
+int vsig_db_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, double floor_, void* out) {
+  if (!c || !a || !out) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  HIPCHK(c, vsig::launch_db_transform(dtype, a, n, floor_, out, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_abs_c64_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, void* out) {
+  if (!c || !a || !out) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  HIPCHK(c, vsig::launch_abs_c64(dtype, a, n, (float2*)out, c->stream));
   return VSIG_OK;
 }
 

@@ -51,4 +51,19 @@ hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
                                    PeakPartial* out, hipStream_t st);
 
+// analysis.hip
+hipError_t launch_radix_hist(int dtype, const void* a, long long n, const unsigned long long* prefix,
+                             const unsigned long long* mask, int nq, int shift,
+                             unsigned long long* hist, hipStream_t st);
+struct ThreshPartialH { long long count, first, last; double max; };   // = ThreshPartial
+hipError_t launch_thresh_reduce(int dtype, const void* a, long long n, double thr, void* parts,
+                                int nparts, hipStream_t st);
+long long energy_scan_tiles(long long n);
+hipError_t launch_energy_prefix(int dtype, const void* x, long long n, double* sums, double* P,
+                                hipStream_t st);
+hipError_t launch_boxcar_same(const double* P, long long n, long long w, double* sm, hipStream_t st);
+hipError_t launch_db_transform(int dtype, const void* a, long long n, double floor_, void* out,
+                               hipStream_t st);
+hipError_t launch_abs_c64(int dtype, const void* a, long long n, float2* out, hipStream_t st);
+
 }  // namespace vsig

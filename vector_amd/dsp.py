@@ -398,6 +398,9 @@ def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
     if mode == "full":
         lag = np.int64(idx - (l1 - 1))
     elif mode == "valid":
+        if idx >= l2 - l1 + 1:          # lag axis np.arange(l2 - l1 + 1) (utils.py:1291)
+            raise IndexError(f"index {idx} is out of bounds for axis 0 with size "
+                             f"{max(0, l2 - l1 + 1)}")
         lag = np.int64(idx)
     else:
         lag = _lags(mode, l1, l2)[idx]      # raises IndexError like the reference
