@@ -145,6 +145,15 @@ int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, 
 int vsig_peak_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev);
 int vsig_peak(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak);
 
+/* ---- polyphase channelizer (BASELINE config 4; no reference counterpart,
+ * nearest analogue vector_analyzer/split_channels.py:15-44):
+ * y[m*nchan + k] = sum_p z_m[p] e^{-2 pi j k p / nchan},
+ * z_m[p] = sum_q h[q*nchan + p] x[(m + q)*nchan + p];
+ * nchan in {64, 128, 256}, ntaps = {4, 8, 16} * nchan,
+ * nframes = (n - ntaps) / nchan + 1; y frame-major (nframes x nchan). */
+int vsig_pfb_c64_dev(vsig_ctx* ctx, const void* x, int64_t n, const float* h, int32_t ntaps,
+                     int32_t nchan, void* y, int64_t nframes);
+
 /* ---- analysis (normalize_spectrogram utils.py:356-404, find_packet_start /
  * detect_packet_bounds utils.py:784-825).  All operate on |a|.
  * vsig_select_dev: k-th smallest |a| for up to 4 0-based ranks (host output;

@@ -1,0 +1,118 @@
+// Critically sampled polyphase filter-bank analysis channelizer (BASELINE
+// config 4; no reference counterpart — the nearest analogue is the FFT
+// brick-wall split vector_analyzer/split_channels.py:15-44; definition in
+// oracle/ref.py pfb_channelize):
+//
+//   z_m[p]  = sum_{q<PT} h[q*C + p] * x[m*C + q*C + p]        (windowed pre-sum)
+//   Y[m, k] = sum_{p<C} z_m[p] * exp(-2j*pi*k*p/C)             (C-point FFT)
+//
+// One block = 256 threads = G = 256/C groups of C lanes; lane p of a group
+// owns branch p and walks the group's frames in order, keeping the PT input
+// rows of the current frame in a register ring (one coalesced row load per
+// frame: every input sample is read from HBM once).  Every E frames of every
+// group (256*E/C frames, 256*E points) the pre-sums go through LDS into the
+// in-LDS Stockham engine (fft_engine.hpp, TF = C/E threads per frame) and the
+// spectra are written frame-major: y[m*C + k] (the (C, M) result is the
+// transposed view, as spectrum() returns Sxx).
+//
+// HBM: 8 B in + 8 B out per input sample (critically sampled).
+#include <hip/hip_runtime.h>
+
+#include "fft_engine.hpp"
+#include "vsig_kernels.h"
+
+namespace vsig {
+
+constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
+
+template <class PL, int PT>
+__global__ __launch_bounds__(256) void pfb_kernel(const float2* __restrict__ x, long long n,
+                                                  const float* __restrict__ h, long long M,
+                                                  long long fpg, float2* __restrict__ y,
+                                                  const float2* __restrict__ tw) {
+  constexpr int C = PL::N, E = PL::E, TF = PL::TF, G = 256 / C;
+  constexpr int U = PT / cgcd(E, PT);          // batches per ring period
+  static_assert(G * E * TF == 256, "one FFT thread per (frame, t) of a batch");
+  __shared__ float2 lds[G * E * PL::LDS];
+  const int tid = threadIdx.x, p = tid % C, g = tid / C;
+  float hq[PT];
+#pragma unroll
+  for (int q = 0; q < PT; ++q) hq[q] = h[q * C + p];
+  const long long gid = (long long)blockIdx.x * G + g;       // this lane's group
+  const long long m0 = gid * fpg;
+  auto row = [&](long long m) -> float2 {                     // x[m*C + p] or 0
+    const long long i = m * C + p;
+    return i < n ? x[i] : make_float2(0.f, 0.f);
+  };
+  float2 ring[PT];
+#pragma unroll
+  for (int q = 0; q < PT - 1; ++q) ring[q] = row(m0 + q);
+  // FFT role of this thread: frame slot ff of the batch, thread t of the frame
+  const int ff = tid / TF, t = tid % TF;
+  const long long mout0 = ((long long)blockIdx.x * G + ff / E) * fpg + ff % E;
+  float2* fl = lds + ff * PL::LDS;
+  for (long long b = 0; b < fpg; b += (long long)E * U) {
+    static_for<0, U>([&](auto ui) {
+      constexpr int u = decltype(ui)::value;
+      static_for<0, E>([&](auto ii) {
+        constexpr int i = decltype(ii)::value;
+        constexpr int k = u * E + i;                          // frame index mod ring
+        const long long m = m0 + b + k;
+        ring[(k + PT - 1) % PT] = row(m + PT - 1);
+        float2 z = make_float2(0.f, 0.f);
+        static_for<0, PT>([&](auto qi) {
+          constexpr int q = decltype(qi)::value;
+          z.x = fmaf(hq[q], ring[(k + q) % PT].x, z.x);
+          z.y = fmaf(hq[q], ring[(k + q) % PT].y, z.y);
+        });
+        lds[(g * E + i) * PL::LDS + lpad(p)] = z;
+      });
+      __syncthreads();
+      float2 v[E];
+      fft_load<PL, 0>(v, fl, t);
+      fft_frame<PL>(v, fl, tw, t);
+      const long long m = mout0 + b + u * E;
+      if (m < M && b + u * E + ff % E < fpg) {
+        float2* yo = y + m * C;
+#pragma unroll
+        for (int e = 0; e < E; ++e) yo[out_index<PL>(t, e)] = v[e];
+      }
+      __syncthreads();                                        // lds reused by the next batch
+    });
+  }
+}
+
+template <class PL, int PT>
+static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
+                         const float2* tw, hipStream_t st) {
+  constexpr int G = 256 / PL::N, E = PL::E;
+  constexpr int step = E * (PT / cgcd(E, PT));
+  // frames per group: a multiple of the unrolled step, ~128 frames so the
+  // (PT-1)-row ring prologue stays a small fraction of the group's reads
+  const long long fpg = ((128 + step - 1) / step) * step;
+  const long long groups = (M + fpg - 1) / fpg;
+  const long long blocks = (groups + G - 1) / G;
+  hipLaunchKernelGGL((pfb_kernel<PL, PT>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M, fpg,
+                     y, tw);
+}
+
+hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
+                      float2* y, const float2* tw, hipStream_t st) {
+#define VSIG_PFB_CASE(CC, PL)                                              \
+  if (C == CC) {                                                           \
+    switch (PT) {                                                          \
+      case 4: launch_pfb_t<PL, 4>(x, n, h, M, y, tw, st); break;           \
+      case 8: launch_pfb_t<PL, 8>(x, n, h, M, y, tw, st); break;           \
+      case 16: launch_pfb_t<PL, 16>(x, n, h, M, y, tw, st); break;         \
+      default: return hipErrorInvalidValue;                                \
+    }                                                                      \
+    return hipGetLastError();                                              \
+  }
+  VSIG_PFB_CASE(64, Plan64)
+  VSIG_PFB_CASE(128, Plan128)
+  VSIG_PFB_CASE(256, Plan256)
+#undef VSIG_PFB_CASE
+  return hipErrorInvalidValue;
+}
+
+}  // namespace vsig

@@ -621,6 +621,25 @@ int vsig_peak(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, vsig_peak_t*
   return VSIG_OK;
 }
 
+// ---------------------------------------------------------------- PFB
+int vsig_pfb_c64_dev(vsig_ctx* c, const void* x, int64_t n, const float* h, int32_t ntaps,
+                     int32_t nchan, void* y, int64_t nframes) {
+  if (!c || !x || !h || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (nchan != 64 && nchan != 128 && nchan != 256)
+    return fail(c, VSIG_E_UNSUPPORTED, "nchan must be 64, 128 or 256");
+  const int pt = ntaps / nchan;
+  if (ntaps % nchan || (pt != 4 && pt != 8 && pt != 16))
+    return fail(c, VSIG_E_UNSUPPORTED, "ntaps must be 4, 8 or 16 times nchan");
+  if (n < ntaps) return fail(c, VSIG_E_INVALID, "signal shorter than the prototype filter");
+  if (nframes != (n - ntaps) / nchan + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
+  const float2* tw;
+  int rc = get_twiddles(c, nchan, &tw);
+  if (rc) return rc;
+  Timed t(c, "pfb");
+  HIPCHK(c, vsig::launch_pfb(nchan, pt, (const float2*)x, n, h, nframes, (float2*)y, tw, c->stream));
+  return VSIG_OK;
+}
+
 // ---------------------------------------------------------------- analysis
 // k-th smallest of |a| (0-based ranks) by MSB-first 8-bit radix select:
 // ceil(bits/8) histogram passes over the data, all ranks at once.

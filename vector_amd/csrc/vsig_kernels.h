@@ -51,6 +51,10 @@ hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
                                    PeakPartial* out, hipStream_t st);
 
+// pfb.hip: C in {64, 128, 256}, PT in {4, 8, 16}; y frame-major (M x C)
+hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
+                      float2* y, const float2* tw, hipStream_t st);
+
 // analysis.hip
 hipError_t launch_radix_hist(int dtype, const void* a, long long n, const unsigned long long* prefix,
                              const unsigned long long* mask, int nq, int shift,
