@@ -145,3 +145,59 @@ def test_chain_config_validation():
         ChainConfig(n_local=1024, taps=np.ones(3), decim=1, nfft=1000).validate(2)
     with pytest.raises(ValueError):
         ChainConfig(n_local=128, taps=np.ones(3), nfft=64, template=np.ones(500)).validate(2)
+
+
+# ---------------------------------------------------------------- sharded PFB (config 4)
+class OraclePfbBackend:
+    """CPU stand-in for HipPfbBackend (test infrastructure)."""
+
+    def __init__(self, proto, C):
+        self.h, self.C = proto, C
+
+    def empty(self, n, dtype=torch.complex64):
+        return torch.zeros(n, dtype=dtype)
+
+    def pfb_into(self, x, y):
+        Y = ref.pfb_channelize(x.numpy(), self.h, self.C)          # (C, nf)
+        y[: Y.size].copy_(torch.from_numpy(np.ascontiguousarray(Y.T).ravel()))
+
+
+def _pfb_worker(rank, world, port, n_local, C, P, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from vector_amd.shard import PfbChain
+        h = np.hanning(P * C).astype(np.float32)
+        x = ref.synth_iq(world * n_local, seed=5)
+        ch = PfbChain(n_local, h, C, OraclePfbBackend(h, C), rank, world)
+        ch.x.copy_(torch.from_numpy(x[rank * n_local:(rank + 1) * n_local]))
+        ch.step()
+        q.put((rank, ch.frame0, ch.frames().numpy().copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pfb_matches_single_stream(world):
+    n_local, C, P = 64 * 40, 64, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_pfb_worker, args=(r, world, port, n_local, C, P, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, f0, Y = q.get(timeout=120)
+        res[r] = (f0, Y)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    h = np.hanning(P * C).astype(np.float32)
+    x = ref.synth_iq(world * n_local, seed=5)
+    full = ref.pfb_channelize(x, h, C).T                           # (M, C)
+    cat = np.concatenate([res[r][1] for r in range(world)])
+    assert cat.shape == full.shape
+    np.testing.assert_array_equal(cat, full)
+    assert [res[r][0] for r in range(world)] == [r * n_local // C for r in range(world)]

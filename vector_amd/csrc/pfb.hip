@@ -25,8 +25,14 @@ namespace vsig {
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 
-template <class PL, int PT>
-__global__ __launch_bounds__(256) void pfb_kernel(const float2* __restrict__ x, long long n,
+// VAR bit 0: spectra leave through LDS so every store is a full C-point row
+// (512 B per wave instruction for C = 64) instead of TF-point runs.
+// VAR bit 1: the next batch's E input rows are loaded before this batch's FFT
+// and stores, so their HBM latency overlaps the compute (more bytes in flight
+// per CU for the same occupancy).
+// VAR bit 2: cap registers for 4 waves / SIMD (4 blocks per CU).
+template <class PL, int PT, int VAR>
+__global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float2* __restrict__ x, long long n,
                                                   const float* __restrict__ h, long long M,
                                                   long long fpg, float2* __restrict__ y,
                                                   const float2* __restrict__ tw) {
@@ -47,6 +53,12 @@ __global__ __launch_bounds__(256) void pfb_kernel(const float2* __restrict__ x, 
   float2 ring[PT];
 #pragma unroll
   for (int q = 0; q < PT - 1; ++q) ring[q] = row(m0 + q);
+  constexpr bool PF = (VAR & 2) != 0;
+  float2 nxt[PF ? E : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int i = 0; i < E; ++i) nxt[i] = row(m0 + PT - 1 + i);
+  }
   // FFT role of this thread: frame slot ff of the batch, thread t of the frame
   const int ff = tid / TF, t = tid % TF;
   const long long mout0 = ((long long)blockIdx.x * G + ff / E) * fpg + ff % E;
@@ -58,7 +70,8 @@ __global__ __launch_bounds__(256) void pfb_kernel(const float2* __restrict__ x, 
         constexpr int i = decltype(ii)::value;
         constexpr int k = u * E + i;                          // frame index mod ring
         const long long m = m0 + b + k;
-        ring[(k + PT - 1) % PT] = row(m + PT - 1);
+        if constexpr (PF) ring[(k + PT - 1) % PT] = nxt[i];
+        else ring[(k + PT - 1) % PT] = row(m + PT - 1);
         float2 z = make_float2(0.f, 0.f);
         static_for<0, PT>([&](auto qi) {
           constexpr int q = decltype(qi)::value;
@@ -67,15 +80,32 @@ __global__ __launch_bounds__(256) void pfb_kernel(const float2* __restrict__ x, 
         });
         lds[(g * E + i) * PL::LDS + lpad(p)] = z;
       });
+      if constexpr (PF) {
+        const long long mn = m0 + b + (u + 1) * E + PT - 1;   // next batch's new rows
+#pragma unroll
+        for (int i = 0; i < E; ++i) nxt[i] = row(mn + i);
+      }
       __syncthreads();
       float2 v[E];
       fft_load<PL, 0>(v, fl, t);
       fft_frame<PL>(v, fl, tw, t);
-      const long long m = mout0 + b + u * E;
-      if (m < M && b + u * E + ff % E < fpg) {
-        float2* yo = y + m * C;
+      if constexpr (VAR & 1) {
+        __syncthreads();                                      // last FFT pass read lds
 #pragma unroll
-        for (int e = 0; e < E; ++e) yo[out_index<PL>(t, e)] = v[e];
+        for (int e = 0; e < E; ++e) fl[lpad(out_index<PL>(t, e))] = v[e];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < E; ++i) {
+          const long long m = m0 + b + u * E + i;
+          if (m < M) y[m * C + p] = lds[(g * E + i) * PL::LDS + lpad(p)];
+        }
+      } else {
+        const long long m = mout0 + b + u * E;
+        if (m < M) {
+          float2* yo = y + m * C;
+#pragma unroll
+          for (int e = 0; e < E; ++e) yo[out_index<PL>(t, e)] = v[e];
+        }
       }
       __syncthreads();                                        // lds reused by the next batch
     });
@@ -84,29 +114,39 @@ __global__ __launch_bounds__(256) void pfb_kernel(const float2* __restrict__ x, 
 
 template <class PL, int PT>
 static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
-                         const float2* tw, hipStream_t st) {
+                         const float2* tw, int variant, int fpg_hint, hipStream_t st) {
   constexpr int G = 256 / PL::N, E = PL::E;
   constexpr int step = E * (PT / cgcd(E, PT));
-  // frames per group: a multiple of the unrolled step, ~128 frames so the
-  // (PT-1)-row ring prologue stays a small fraction of the group's reads
-  const long long fpg = ((128 + step - 1) / step) * step;
+  // frames per group: a multiple of the unrolled step, ~128 frames by default
+  // so the (PT-1)-row ring prologue stays a small fraction of the group's reads
+  const int want = fpg_hint > 0 ? fpg_hint : 128;
+  const long long fpg = ((want + step - 1) / step) * step;
   const long long groups = (M + fpg - 1) / fpg;
   const long long blocks = (groups + G - 1) / G;
-  hipLaunchKernelGGL((pfb_kernel<PL, PT>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M, fpg,
-                     y, tw);
+#define VSIG_PFB_GO(V) \
+  hipLaunchKernelGGL((pfb_kernel<PL, PT, V>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M, fpg, y, tw)
+  switch (variant & 7) {
+    case 0: VSIG_PFB_GO(0); break;
+    case 1: VSIG_PFB_GO(1); break;
+    case 2: VSIG_PFB_GO(2); break;
+    case 3: VSIG_PFB_GO(3); break;
+    case 7: VSIG_PFB_GO(7); break;
+    default: VSIG_PFB_GO(3); break;
+  }
+#undef VSIG_PFB_GO
 }
 
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
-                      float2* y, const float2* tw, hipStream_t st) {
-#define VSIG_PFB_CASE(CC, PL)                                              \
-  if (C == CC) {                                                           \
-    switch (PT) {                                                          \
-      case 4: launch_pfb_t<PL, 4>(x, n, h, M, y, tw, st); break;           \
-      case 8: launch_pfb_t<PL, 8>(x, n, h, M, y, tw, st); break;           \
-      case 16: launch_pfb_t<PL, 16>(x, n, h, M, y, tw, st); break;         \
-      default: return hipErrorInvalidValue;                                \
-    }                                                                      \
-    return hipGetLastError();                                              \
+                      float2* y, const float2* tw, int variant, int fpg, hipStream_t st) {
+#define VSIG_PFB_CASE(CC, PL)                                                        \
+  if (C == CC) {                                                                     \
+    switch (PT) {                                                                    \
+      case 4: launch_pfb_t<PL, 4>(x, n, h, M, y, tw, variant, fpg, st); break;       \
+      case 8: launch_pfb_t<PL, 8>(x, n, h, M, y, tw, variant, fpg, st); break;       \
+      case 16: launch_pfb_t<PL, 16>(x, n, h, M, y, tw, variant, fpg, st); break;     \
+      default: return hipErrorInvalidValue;                                          \
+    }                                                                                \
+    return hipGetLastError();                                                        \
   }
   VSIG_PFB_CASE(64, Plan64)
   VSIG_PFB_CASE(128, Plan128)

@@ -32,6 +32,7 @@ struct vsig_ctx {
   std::map<std::string, TimingRec> timers;
   vsig::Variants var{16, 8, 10};         // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
+  int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
 
 struct vsig_fir {
@@ -328,6 +329,11 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
         value != 16384)
       return fail(c, VSIG_E_INVALID, "block size must be 0, 1024, 2048, 4096, 8192 or 16384");
     (k == "fir_m" ? c->fir_m : c->xcorr_m) = value;
+  } else if (k == "pfb_variant") {
+    c->pfb_variant = value & 7;
+  } else if (k == "pfb_fpg") {
+    if (value < 0 || value > 65536) return fail(c, VSIG_E_INVALID, "pfb_fpg must be in [0, 65536]");
+    c->pfb_fpg = value;
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }
@@ -636,7 +642,8 @@ int vsig_pfb_c64_dev(vsig_ctx* c, const void* x, int64_t n, const float* h, int3
   int rc = get_twiddles(c, nchan, &tw);
   if (rc) return rc;
   Timed t(c, "pfb");
-  HIPCHK(c, vsig::launch_pfb(nchan, pt, (const float2*)x, n, h, nframes, (float2*)y, tw, c->stream));
+  HIPCHK(c, vsig::launch_pfb(nchan, pt, (const float2*)x, n, h, nframes, (float2*)y, tw, c->pfb_variant,
+                             c->pfb_fpg, c->stream));
   return VSIG_OK;
 }
 

@@ -53,7 +53,7 @@ hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, i
 
 // pfb.hip: C in {64, 128, 256}, PT in {4, 8, 16}; y frame-major (M x C)
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
-                      float2* y, const float2* tw, hipStream_t st);
+                      float2* y, const float2* tw, int variant, int fpg, hipStream_t st);
 
 // analysis.hip
 hipError_t launch_radix_hist(int dtype, const void* a, long long n, const unsigned long long* prefix,

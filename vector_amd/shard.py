@@ -32,7 +32,8 @@ import numpy as np
 import torch
 import torch.distributed as dist
 
-__all__ = ["ChainConfig", "HipBackend", "StreamChain", "combine_peaks"]
+__all__ = ["ChainConfig", "HipBackend", "StreamChain", "combine_peaks", "HipPfbBackend",
+           "PfbChain"]
 
 
 @dataclass
@@ -249,3 +250,77 @@ class StreamChain:
         m, i, s1, s2 = combine_peaks(np.array(rows, dtype=object))
         nout = self.world * self.ny - self.L + 1
         return m, i, s1, s2, nout
+
+
+# ---------------------------------------------------------------------------
+# Sharded polyphase channelizer (BASELINE config 4)
+# ---------------------------------------------------------------------------
+class HipPfbBackend:
+    """libvsig.so's PFB kernel on the rank's GPU (product backend)."""
+
+    def __init__(self, proto, nchan: int, device: int):
+        from .channelizer import Channelizer
+        self.ch = Channelizer(proto, nchan, device)
+        self.ctx = self.ch.ctx
+        self.dev = torch.device(f"cuda:{device}")
+
+    def empty(self, n, dtype=torch.complex64):
+        return torch.zeros(n, dtype=dtype, device=self.dev)
+
+    def pfb_into(self, x, y):
+        """frames of x (frame-major, nframes x nchan) into the flat buffer y."""
+        C = self.ch.nchan
+        nf = self.ch.nframes(int(x.shape[0]))
+        self.ch(x, out=y[: nf * C].view(nf, C))
+
+
+class PfbChain:
+    """One rank's part of a time-chunk-sharded C-channel PFB.
+
+    Rank r owns X[r*n, (r+1)*n) and the output frames that start in it
+    (frame m reads X[m*C, m*C + ntaps)), so it needs a RIGHT halo of
+    ntaps - C samples: the first samples of rank r+1's chunk, received over
+    RCCL before the kernel runs.  Concatenating the ranks' frames gives the
+    single-stream result exactly ((world*n - ntaps)//C + 1 frames)."""
+
+    def __init__(self, n_local: int, proto, nchan: int, backend, rank: int = 0, world: int = 1,
+                 group=None):
+        C, ntaps = int(nchan), len(proto)
+        if n_local % C:
+            raise ValueError("n_local must be a multiple of nchan (frames never straddle ranks)")
+        if world > 1 and n_local < ntaps - C:
+            raise ValueError("chunk shorter than the PFB halo")
+        self.n, self.C, self.ntaps = n_local, C, ntaps
+        self.be, self.rank, self.world, self.group = backend, rank, world, group
+        self.halo = ntaps - C
+        self.rhalo = self.halo if rank < world - 1 else 0
+        self.nframes = n_local // C if rank < world - 1 else max(0, (n_local - ntaps) // C + 1)
+        self.x_ext = backend.empty(n_local + self.halo)                 # [chunk | right halo]
+        self.y = backend.empty(max(self.nframes, 1) * C)                # frame-major
+
+    @property
+    def x(self):
+        return self.x_ext[: self.n]
+
+    @property
+    def frame0(self):
+        """Global index of this rank's first frame."""
+        return self.rank * (self.n // self.C)
+
+    def step(self):
+        r, w, h = self.rank, self.world, self.halo
+        if w > 1 and h > 0:
+            ops = []
+            if r > 0:
+                ops.append(dist.P2POp(dist.isend, self.x_ext[:h], r - 1, group=self.group))
+            if r < w - 1:
+                ops.append(dist.P2POp(dist.irecv, self.x_ext[self.n: self.n + h], r + 1,
+                                      group=self.group))
+            for req in dist.batch_isend_irecv(ops):
+                req.wait()
+        if self.nframes > 0:
+            self.be.pfb_into(self.x_ext[: self.n + self.rhalo], self.y)
+
+    def frames(self):
+        """(nframes, C) view of this rank's output."""
+        return self.y[: self.nframes * self.C].view(self.nframes, self.C)
