@@ -17,6 +17,7 @@ import sys
 from collections import defaultdict
 
 FAMILY = {"fir_os_kernel": "fir", "psd_kernel": "psd", "xcorr_os_kernel": "xcorr",
+          "xcorr_part_kernel": "xcorr", "pfb_kernel": "pfb",
           "peak_reduce": "peak", "partial_finalize": "finalize"}
 
 
@@ -65,6 +66,9 @@ def main(src, dst, keyspec):
             rec = {"config_key": f"{fam}:{keyspec}", "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
                    "source": f"{os.path.basename(dst)} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"}
             out["kernels"][fam]["bench_record"] = rec
+            tag = os.path.basename(dst)[len("pmc_"):] if os.path.basename(dst).startswith("pmc_") \
+                else os.path.basename(dst)
+            json.dump(rec, open(os.path.join(os.path.dirname(dst), f"pmc_{fam}_{tag}"), "w"), indent=1)
     json.dump(out, open(dst, "w"), indent=1)
     for fam, d in out["kernels"].items():
         print(fam, {k: (round(v, 3) if isinstance(v, float) else v) for k, v in d.items() if k != "counters"})

@@ -24,22 +24,27 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    """Compile every HIP source into vector_amd/libvsig.so (gfx950)."""
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = True, defines=(), out: str = LIB) -> str:
+    """Compile every HIP source into vector_amd/libvsig.so (gfx950).  `defines`
+    / `out` build A/B variants (e.g. VSIG_SCALAR_FFT -> libvsig_scalar.so,
+    loaded with VSIG_LIB=... by the tuning tools; never by the product)."""
+    if out == LIB and not defines and not force and not _stale():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    tmp = LIB + ".tmp"
+    tmp = out + ".tmp"
     cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
            "-fno-slp-vectorize",   # SLP packs f32 pairs into v_pk_* + v_mov shuffles
-           "-Wall", "-Wno-unused-function",
+           "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines],
            *[os.path.join(CSRC, s) for s in SOURCES], "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)
     subprocess.run(cmd, check=True)
-    os.replace(tmp, LIB)
-    return LIB
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    build(force="--force" in sys.argv)
+    if "--scalar" in sys.argv:
+        build(defines=("VSIG_SCALAR_FFT",), out=os.path.join(HERE, "libvsig_scalar.so"))
+    else:
+        build(force="--force" in sys.argv)

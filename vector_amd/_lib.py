@@ -76,9 +76,11 @@ _lib = None
 _lib_lock = threading.Lock()
 
 
-def load_library(path: str = LIB_PATH):
-    """Load libvsig.so and declare every entry point; no device needed."""
+def load_library(path: str | None = None):
+    """Load libvsig.so and declare every entry point; no device needed.
+    (VSIG_LIB selects an A/B build of the same sources, for the tuning tools.)"""
     global _lib
+    path = path or os.environ.get("VSIG_LIB") or LIB_PATH
     with _lib_lock:
         if _lib is not None:
             return _lib

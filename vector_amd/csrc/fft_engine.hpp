@@ -30,11 +30,74 @@
 
 namespace vsig {
 
+// Complex arithmetic.  CDNA3/4 execute packed fp32 (v_pk_add/mul/fma_f32) at
+// the scalar rate, so a complex value in an (even-aligned) VGPR pair costs one
+// instruction per add and two per multiply when the operand swizzles go into
+// the VOP3P op_sel / neg modifiers — which the compiler does not do on its own
+// for swizzled operands, hence the inline asm below.  Build with
+// -DVSIG_SCALAR_FFT for the plain two-lane scalar form (A/B reference).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v tov(float2 a) { return (f2v){a.x, a.y}; }
+__device__ __forceinline__ float2 fromv(f2v a) { return make_float2(a.x, a.y); }
+
+#ifndef VSIG_SCALAR_FFT
+#define VSIG_PK 1
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return fromv(tov(a) + tov(b)); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return fromv(tov(a) - tov(b)); }
+// a * b = b.x * (a.x, a.y) + b.y * (-a.y, a.x)
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  const f2v av = tov(a), bv = tov(b);
+  const f2v t = av * bv.xx;
+  f2v r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(av), "v"(bv), "v"(t));
+  return fromv(r);
+}
+// a + (-i) b = (a.x + b.y, a.y - b.x)   and   a - (-i) b = (a.x - b.y, a.y + b.x)
+__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_hi:[0,1]"
+      : "=v"(r) : "v"(tov(a)), "v"(tov(b)));
+  return fromv(r);
+}
+__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 op_sel:[0,1] op_sel_hi:[1,0] neg_lo:[0,1]"
+      : "=v"(r) : "v"(tov(a)), "v"(tov(b)));
+  return fromv(r);
+}
+// a + h * u with a compile-time scalar h (SGPR pair (h, h))
+__device__ __forceinline__ float2 cfma_s(float2 u, float h, float2 a) {
+  f2v r;
+  const f2v hh = (f2v){h, h};
+  asm("v_pk_fma_f32 %0, %1, %2, %3" : "=v"(r) : "v"(tov(u)), "s"(hh), "v"(tov(a)));
+  return fromv(r);
+}
+// b * (c - i s) for compile-time c, s: c * (b.x, b.y) + s * (b.y, -b.x)
+__device__ __forceinline__ float2 cmul_cs(float2 b, float c, float s_) {
+  const f2v bv = tov(b);
+  const f2v cc = (f2v){c, c}, ss = (f2v){s_, s_};
+  f2v t, r;
+  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(t) : "v"(bv), "s"(cc));
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+      : "=v"(r) : "v"(bv), "s"(ss), "v"(t));
+  return fromv(r);
+}
+#else
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
 __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
   return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
 }
+__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
+__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
+__device__ __forceinline__ float2 cfma_s(float2 u, float h, float2 a) {
+  return make_float2(fmaf(h, u.x, a.x), fmaf(h, u.y, a.y));
+}
+__device__ __forceinline__ float2 cmul_cs(float2 b, float c, float s_) {
+  return make_float2(b.x * c + b.y * s_, b.y * c - b.x * s_);
+}
+#endif
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 
 // cos / sin of 2*pi*k/64, k = 0..31 (enough for every in-register radix <= 64).
@@ -74,8 +137,7 @@ __device__ __forceinline__ float2 twc(float2 b) {
     return make_float2(h * (b.y - b.x), -h * (b.x + b.y));
   } else {
     constexpr int idx = K * (64 / M);
-    constexpr float c = kCos64[idx], s = kSin64[idx];
-    return make_float2(b.x * c + b.y * s, b.y * c - b.x * s);
+    return cmul_cs(b, kCos64[idx], kSin64[idx]);
   }
 }
 
@@ -87,9 +149,29 @@ struct Radix2Step {
     constexpr int k = J & (Ns - 1);
     constexpr int o = ((J >> P) << (P + 1)) + k;
     const float2 x0 = a[J];
-    const float2 x1 = twc<k, 2 * Ns>(a[J + R / 2]);
-    t[o] = cadd(x0, x1);
-    t[o + Ns] = csub(x0, x1);
+    const float2 b = a[J + R / 2];
+    constexpr int M = 2 * Ns;
+    if constexpr (k == 0) {
+      t[o] = cadd(x0, b);
+      t[o + Ns] = csub(x0, b);
+    } else if constexpr (4 * k == M) {           // (-i) b folded into the adds
+      t[o] = cadd_mi(x0, b);
+      t[o + Ns] = csub_mi(x0, b);
+    } else if constexpr (8 * k == M) {           // h (b.x + b.y, b.y - b.x)
+      constexpr float h = 7.071067812e-01f;
+      const float2 u = cadd_mi(b, b);
+      t[o] = cfma_s(u, h, x0);
+      t[o + Ns] = cfma_s(u, -h, x0);
+    } else if constexpr (8 * k == 3 * M) {       // -h (b.x - b.y, b.x + b.y)
+      constexpr float h = 7.071067812e-01f;
+      const float2 u = csub_mi(b, b);
+      t[o] = cfma_s(u, -h, x0);
+      t[o + Ns] = cfma_s(u, h, x0);
+    } else {
+      const float2 x1 = twc<k, M>(b);
+      t[o] = cadd(x0, x1);
+      t[o + Ns] = csub(x0, x1);
+    }
     if constexpr (J + 1 < R / 2) Radix2Step<R, P, J + 1>::run(a, t);
   }
 };
