@@ -44,7 +44,8 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
   float hq[PT];
 #pragma unroll
   for (int q = 0; q < PT; ++q) hq[q] = h[q * C + p];
-  const long long gid = (long long)blockIdx.x * G + g;       // this lane's group
+  const long long blk = xcd_remap(blockIdx.x, gridDim.x);   // contiguous runs per XCD
+  const long long gid = blk * G + g;                          // this lane's group
   const long long m0 = gid * fpg;
   auto row = [&](long long m) -> float2 {                     // x[m*C + p] or 0
     const long long i = m * C + p;
@@ -61,7 +62,7 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
   }
   // FFT role of this thread: frame slot ff of the batch, thread t of the frame
   const int ff = tid / TF, t = tid % TF;
-  const long long mout0 = ((long long)blockIdx.x * G + ff / E) * fpg + ff % E;
+  const long long mout0 = (blk * G + ff / E) * fpg + ff % E;
   float2* fl = lds + ff * PL::LDS;
   for (long long b = 0; b < fpg; b += (long long)E * U) {
     static_for<0, U>([&](auto ui) {

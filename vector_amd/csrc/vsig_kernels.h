@@ -4,6 +4,23 @@
 
 namespace vsig {
 
+// XCD-aware block order.  The dispatcher hands block b to XCD b % 8 and each
+// XCD has its own L2, so with the identity mapping the overlap two
+// neighbouring overlap-save segments share is fetched from HBM by two
+// different L2s.  Remapping gives every XCD one contiguous run of segments
+// (a bijection on [0, nb)), so the overlap of b and its successor (dispatched
+// at about the same time to the same XCD) hits in L2.
+__device__ __forceinline__ long long xcd_remap(long long b, long long nb) {
+#ifdef VSIG_NO_XCD_REMAP
+  (void)nb;
+  return b;
+#else
+  const long long q = nb >> 3, r = nb & 7;
+  const long long x = b & 7, i = b >> 3;
+  return x * q + (x < r ? x : r) + i;
+#endif
+}
+
 enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
 
 // One block's |c| reduction partial (also the layout of the final result).
