@@ -408,6 +408,53 @@ __device__ __forceinline__ void block_partial(double m, long long mi, double s1,
   }
 }
 
+// Partials of the correlators: float |c|^2 / int block-local index / float
+// sums, wave-reduced with DPP (VALU-rate lane moves instead of a chain of
+// ds_bpermute round trips and a block barrier — a block's tail is exposed at
+// one block per CU), one partial per wave.  rev: ties go to the larger index.
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RM, 0xf, false));
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ void peak_dpp_step(float& m, int& mi, float& s1, float& s2, bool rev) {
+  const float om = dpp_f<CTRL, RM>(m);
+  const int oi = dpp_i<CTRL, RM>(mi);
+  const bool take = (om > m) | ((om == m) & (rev ? oi > mi : oi < mi));
+  m = take ? om : m;
+  mi = take ? oi : mi;
+  s1 += dpp_f<CTRL, RM>(s1);
+  s2 += dpp_f<CTRL, RM>(s2);
+}
+
+// One partial per wave (no block barrier at the block's tail): lane 63 holds
+// the wave's result after the DPP steps and writes it.
+__device__ __forceinline__ void wave_partial_f(float m, int mi, float s1, float s2, bool rev,
+                                               long long ob, long long nout, PeakPartial* out) {
+  // rocPRIM-style wave64 reduction: quad xor 1, 2; row_ror 4, 8; row_bcast 15, 31
+  // -> lane 63 holds the wave's result (rows not feeding it hold garbage).
+  peak_dpp_step<0xb1, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x4e, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x124, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x128, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x142, 0xa>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x143, 0xc>(m, mi, s1, s2, rev);
+  if ((threadIdx.x & 63) == 63) {
+    long long gi = ob + mi;
+    if (rev) gi = nout - 1 - gi;
+    PeakPartial r;
+    r.max2 = (double)m;
+    r.idx = gi;
+    r.sum_abs = (double)s1;
+    r.sum_abs2 = (double)s2;
+    *out = r;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Cross-correlation, overlap-save:  c[o] = sum_{k<L} s[o - off + k] * conj(p[k]),
 // o in [0, nout).  off = 0 -> np.correlate 'valid'; off = L-1 -> 'full'.
@@ -428,27 +475,39 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
   const int lim = rem < hop ? (int)rem : (int)hop;
   const bool rev = store_mode & 4;
   const int smode = store_mode & 3;
-  float m = -1.f;
-  int mi = rev ? -1 : 0x7fffffff;
-  float s1 = 0.f, s2 = 0.f;
+  // optional store: one uniform branch outside the element loops
+  if (smode == 1) {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e);
+      if (i < lim) (c + ob)[(unsigned)i] = cconj(v[e]);
+    }
+  } else if (smode == 2) {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e);
+      if (i < lim) (c + (nout - 1 - ob))[-i] = v[e];
+    }
+  }
+  if (!partials) return;
+  // branch-free peak / sums.  A thread's output indices rise with e, so a
+  // strict '>' keeps the first maximum; in the reversed index space (rev)
+  // '>=' keeps the last raw index, i.e. the first reversed one.
+  float m = -1.f, s1 = 0.f, s2 = 0.f;
+  int mi = 0;
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = out_index<P>(t, e);
-    if (i < lim) {
-      const float2 cv = cconj(v[e]);
-      const float a2 = cv.x * cv.x + cv.y * cv.y;
-      if (a2 > m || (a2 == m && (rev ? i > mi : i < mi))) { m = a2; mi = i; }
-      s1 += sqrtf(a2);
-      s2 += a2;
-      if (smode == 1) (c + ob)[(unsigned)i] = cv;
-      else if (smode == 2) (c + (nout - 1 - ob))[-i] = cconj(cv);
-    }
+    const bool ok = i < lim;
+    const float a2r = v[e].x * v[e].x + v[e].y * v[e].y;
+    const float a2 = ok ? a2r : -1.f;
+    const bool take = (a2 > m) | (rev & (a2 == m) & ok);
+    m = take ? a2 : m;
+    mi = take ? i : mi;
+    s1 += ok ? __builtin_amdgcn_sqrtf(a2r) : 0.f;   // v_sqrt_f32 (1 ulp), not the IEEE expansion
+    s2 += ok ? a2r : 0.f;
   }
-  if (partials) {
-    long long gi = ob + mi;
-    if (rev) gi = m < 0.f ? 0x7fffffffffffffffll : nout - 1 - gi;
-    block_partial<BT>((double)m, gi, (double)s1, (double)s2, partials + b);
-  }
+  wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (BT / 64) + (t >> 6));
 }
 
 template <class P, int PERSIST>
@@ -481,12 +540,29 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void xc
     float2* t2 = lds + P::LDS;
     load_tw2<P>(t2, tw, t, BT);
     float2 v[P::E];
+#ifdef VSIG_EXP_NO_LOAD      // timing experiments only (results are wrong)
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = make_float2((float)(t + e), (float)(b & 7));
+#else
     load_segment<P>(v, s, b * hop - off, n, t);
+#endif
     fft_frame_t2<P>(v, lds, t2, t);
+#ifdef VSIG_EXP_NO_PS
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), make_float2(0.5f, 0.25f));
+#else
 #pragma unroll
     for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
+#endif
     fft_frame_t2<P>(v, lds, t2, t);
+#ifdef VSIG_EXP_NO_EPI
+    float acc = 0.f;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) acc += v[e].x + v[e].y;
+    if (acc == 12345.f) partials[b].sum_abs = acc;
+#else
     xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
+#endif
     return;
   }
   if constexpr (!PERSIST) {          // one unit per block, table twiddles
@@ -685,6 +761,24 @@ __global__ __launch_bounds__(1024) void partial_finalize(const PeakPartial* __re
   }
 }
 
+// First level of a large reduction: block k reduces the fixed chunk
+// [k*chunk, (k+1)*chunk) into tmp[k] (fixed order -> reproducible).
+__global__ __launch_bounds__(256) void partial_chunks(const PeakPartial* __restrict__ parts,
+                                                      long long nparts, long long chunk,
+                                                      PeakPartial* __restrict__ tmp) {
+  const long long lo = (long long)blockIdx.x * chunk;
+  const long long hi = lo + chunk < nparts ? lo + chunk : nparts;
+  double m = -1.0, s1 = 0.0, s2 = 0.0;
+  long long mi = 0x7fffffffffffffffLL;
+  for (long long i = lo + threadIdx.x; i < hi; i += 256) {
+    const PeakPartial p = parts[i];
+    betterd(m, mi, p.max2, p.idx);
+    s1 += p.sum_abs;
+    s2 += p.sum_abs2;
+  }
+  block_partial<256>(m, mi, s1, s2, tmp + blockIdx.x);
+}
+
 // ---------------------------------------------------------------------------
 // Host-side launchers (called from vsig_api.hip), dispatching N to plans.
 // ---------------------------------------------------------------------------
@@ -855,9 +949,29 @@ hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial
 }
 
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
-                                   PeakPartial* out, hipStream_t st) {
-  hipLaunchKernelGGL(partial_finalize, dim3(1), dim3(1024), 0, st, parts, nparts, sqrt_max, out);
+                                   PeakPartial* out, PeakPartial* tmp, hipStream_t st) {
+  if (nparts > 8192 && tmp) {       // two levels: chunks in parallel, then one block
+    long long g1 = (nparts + 2047) / 2048;
+    if (g1 > kFinalizeTmp) g1 = kFinalizeTmp;
+    const long long chunk = (nparts + g1 - 1) / g1;
+    g1 = (nparts + chunk - 1) / chunk;
+    hipLaunchKernelGGL(partial_chunks, dim3((unsigned)g1), dim3(256), 0, st, parts, nparts, chunk, tmp);
+    hipLaunchKernelGGL(partial_finalize, dim3(1), dim3(1024), 0, st, tmp, g1, sqrt_max, out);
+  } else {
+    hipLaunchKernelGGL(partial_finalize, dim3(1), dim3(1024), 0, st, parts, nparts, sqrt_max, out);
+  }
   return hipGetLastError();
+}
+
+int os_waves(int M, int variant) {
+  switch (M) {
+    case 1024: return os_threads<Plan1024s>() / 64;
+    case 2048: return os_threads<Plan2048s>() / 64;
+    case 4096: return os_threads<Plan4096>() / 64;
+    case 8192: return os_threads<Plan8192>() / 64;
+    case 16384: return (variant & 2) ? os_threads<Plan16384w>() / 64 : os_threads<Plan16384>() / 64;
+    default: return 0;
+  }
 }
 
 }  // namespace vsig

@@ -137,7 +137,8 @@ int ensure_partials(vsig_ctx* c, long long n) {
   c->partials = nullptr;
   c->npartials = 0;
   long long cap = n < 4096 ? 4096 : n + n / 4;
-  HIPCHK(c, hipMalloc(&c->partials, cap * sizeof(PeakPartial)));
+  // + the first-level buffer of a two-level finalize, right after the partials
+  HIPCHK(c, hipMalloc(&c->partials, (cap + vsig::kFinalizeTmp) * sizeof(PeakPartial)));
   c->npartials = cap;
   return VSIG_OK;
 }
@@ -222,7 +223,8 @@ int make_spectrum(vsig_ctx* c, const float2* u_dev, int len, int M, float2** out
 
 int finalize_peak(vsig_ctx* c, long long nparts, int sqrt_max, vsig_peak_t* peak_dev) {
   PeakPartial* dst = peak_dev ? reinterpret_cast<PeakPartial*>(peak_dev) : c->result;
-  HIPCHK(c, vsig::launch_partial_finalize(c->partials, nparts, sqrt_max, dst, c->stream));
+  HIPCHK(c, vsig::launch_partial_finalize(c->partials, nparts, sqrt_max, dst,
+                                          c->partials + c->npartials, c->stream));
   return VSIG_OK;
 }
 
@@ -234,10 +236,11 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, co
   if (nout <= 0) return fail(c, VSIG_E_INVALID, "empty correlation output");
   const long long hop = Ps1 ? (long long)M / 2 : (long long)M - L + 1;
   const long long nblocks = (nout + hop - 1) / hop;
-  int rc = ensure_partials(c, nblocks);
+  const int var = Ps1 ? (c->var.xcorr & 8) : c->var.xcorr;
+  const long long nparts = nblocks * vsig::os_waves(M, var);   // one partial per wave
+  int rc = ensure_partials(c, nparts);
   if (rc) return rc;
   const float2* tw;
-  const int var = Ps1 ? (c->var.xcorr & 8) : c->var.xcorr;
   rc = get_tw_for(c, M, var, true, &tw);
   if (rc) return rc;
   {
@@ -249,7 +252,7 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, co
       HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
                                       c->partials, tw, c->var.xcorr, c->stream));
   }
-  return finalize_peak(c, nblocks, 1, peak_dev);
+  return finalize_peak(c, nparts, 1, peak_dev);
 }
 
 }  // namespace

@@ -65,8 +65,10 @@ hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const fl
                             hipStream_t st);
 hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
                               int nparts, hipStream_t st);
+constexpr int kFinalizeTmp = 1024;   // first-level partials of a two-level finalize
+int os_waves(int M, int variant);    // waves per overlap-save block (partials per unit)
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
-                                   PeakPartial* out, hipStream_t st);
+                                   PeakPartial* out, PeakPartial* tmp, hipStream_t st);
 
 // pfb.hip: C in {64, 128, 256}, PT in {4, 8, 16}; y frame-major (M x C)
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
