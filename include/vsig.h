@@ -145,6 +145,27 @@ int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, 
 int vsig_peak_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev);
 int vsig_peak(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak);
 
+/* ---- stream ops either side of the chain.
+ * vsig_mix_c64_dev: y[i] = x[i] * exp(j w (i0 + i) / sr) — apply_frequency_shift
+ *   (utils.py:120-127) with w = 2*pi*freq_shift as numpy forms it.
+ * vsig_scale_c64_dev: y = x * s (transplant_packet_in_vector power scale,
+ *   utils.py:1481-1496).
+ * vsig_wv_quantize_dev: SMU-WV int16 I/Q interleave of mat2wv
+ *   (vector_analyzer/mat_to_wv_converter.py:28-50); norm > 0 divides by norm
+ *   first (bNormalize, norm = max |x|); out holds 2n int16.
+ * vsig_planar_to_c64_dev: MAT v5 real / imaginary planes of storage type
+ *   mi_type (miINT8 1 .. miDOUBLE 9, miINT64 12, miUINT64 13; im may be NULL)
+ *   -> complex64 (load_packet, utils.py:48-86).
+ * vsig_c64_to_planar_dev: complex64 -> float32 planes (save_vector,
+ *   utils.py:659-670). */
+int vsig_mix_c64_dev(vsig_ctx* ctx, const void* x, int64_t n, double w, double sr, int64_t i0,
+                     void* y);
+int vsig_scale_c64_dev(vsig_ctx* ctx, const void* x, int64_t n, float s, void* y);
+int vsig_wv_quantize_dev(vsig_ctx* ctx, const void* x, int64_t n, float norm, int16_t* out);
+int vsig_planar_to_c64_dev(vsig_ctx* ctx, int32_t mi_type, const void* re, const void* im,
+                           int64_t n, void* y);
+int vsig_c64_to_planar_dev(vsig_ctx* ctx, const void* x, int64_t n, float* re, float* im);
+
 /* ---- polyphase channelizer (BASELINE config 4; no reference counterpart,
  * nearest analogue vector_analyzer/split_channels.py:15-44):
  * y[m*nchan + k] = sum_p z_m[p] e^{-2 pi j k p / nchan},

@@ -304,6 +304,58 @@ def pfb_channelize(x, proto, nchan):
 
 
 # ---------------------------------------------------------------------------
+# element-wise steps and formats either side of the chain
+# ---------------------------------------------------------------------------
+def apply_frequency_shift(signal, freq_shift, sample_rate):
+    """utils.py:120-127."""
+    if freq_shift == 0:
+        return signal
+    t = np.arange(len(signal)) / sample_rate
+    shift_factor = np.exp(2j * np.pi * freq_shift * t)
+    return (signal * shift_factor).astype(np.complex64)
+
+
+def transplant_packet_in_vector(vector, packet_signal, vector_location, packet_location=0,
+                                replace_length=None, normalize_power=True):
+    """utils.py:1437-1501 (prints omitted)."""
+    new_vector = vector.copy()
+    if replace_length is None:
+        replace_length = len(packet_signal) - packet_location
+    vector_end = min(vector_location + replace_length, len(vector))
+    actual_replace_length = vector_end - vector_location
+    packet_end = min(packet_location + actual_replace_length, len(packet_signal))
+    actual_packet_length = packet_end - packet_location
+    if vector_location >= 0 and vector_location < len(vector) and actual_packet_length > 0:
+        seg = packet_signal[packet_location:packet_location + actual_packet_length]
+        if normalize_power:
+            orig = vector[vector_location:vector_location + actual_packet_length]
+            op = np.mean(np.abs(orig) ** 2)
+            pp = np.mean(np.abs(seg) ** 2)
+            if pp > 0 and op > 0:
+                seg = seg * np.sqrt(op / pp)
+        new_vector[vector_location:vector_location + actual_packet_length] = seg
+    return new_vector
+
+
+def mat2wv_fields(signal, bNormalize=True):
+    """vector_analyzer/mat_to_wv_converter.py:28-50: (interleaved int16 I/Q,
+    fRMSdBfs, fPeakPowerdBfs) — the SMU-WV payload and level fields."""
+    signal = np.asarray(signal).flatten()
+    if bNormalize:
+        signal = signal / np.max(np.abs(signal))
+        fPeakPowerdBfs = -10 * np.log10(np.max(np.abs(signal) ** 2))
+        fRMSdBfs = -10 * np.log10(np.mean(np.abs(signal) ** 2))
+    else:
+        fPeakPowerdBfs = 0.0
+        fRMSdBfs = 0.0
+    vicData = signal * 32767
+    out = np.empty(2 * signal.size, dtype=np.int16)
+    out[0::2] = np.real(vicData).astype(np.int16)
+    out[1::2] = np.imag(vicData).astype(np.int16)
+    return out, fRMSdBfs, fPeakPowerdBfs
+
+
+# ---------------------------------------------------------------------------
 # synthetic inputs — SURVEY.md §8(d)
 # ---------------------------------------------------------------------------
 TONES = ((1.0, 0.05), (0.5, 0.11), (0.25, -0.20))

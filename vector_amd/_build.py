@@ -10,7 +10,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvsig.so")
-SOURCES = ["kernels.hip", "analysis.hip", "pfb.hip", "vsig_api.hip"]
+SOURCES = ["kernels.hip", "analysis.hip", "pfb.hip", "stream_ops.hip", "vsig_api.hip"]
 HEADERS = ["fft_engine.hpp", "vsig_kernels.h"]
 ARCH = os.environ.get("VSIG_ARCH", "gfx950")
 

@@ -63,6 +63,11 @@ SIGNATURES = {
     "vsig_correlate_c64": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
     "vsig_peak_dev": (C.c_int, [P, I32, P, I64, P]),
     "vsig_peak": (C.c_int, [P, I32, P, I64, P]),
+    "vsig_mix_c64_dev": (C.c_int, [P, P, I64, C.c_double, C.c_double, I64, P]),
+    "vsig_scale_c64_dev": (C.c_int, [P, P, I64, C.c_float, P]),
+    "vsig_wv_quantize_dev": (C.c_int, [P, P, I64, C.c_float, P]),
+    "vsig_planar_to_c64_dev": (C.c_int, [P, I32, P, P, I64, P]),
+    "vsig_c64_to_planar_dev": (C.c_int, [P, P, I64, P, P]),
     "vsig_pfb_c64_dev": (C.c_int, [P, P, I64, P, I32, I32, P, I64]),
     "vsig_select_dev": (C.c_int, [P, I32, P, I64, C.POINTER(I64), I32, C.POINTER(C.c_double)]),
     "vsig_threshold_dev": (C.c_int, [P, I32, P, I64, C.c_double, C.POINTER(I64), C.POINTER(I64),

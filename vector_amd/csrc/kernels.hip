@@ -18,7 +18,13 @@ namespace vsig {
 // exchange (variant 4) exists to fit two 16k / four 8k frames per CU, which
 // needs <= 128 VGPRs, so ask the register allocator for 4 waves/SIMD there.
 template <class P, int PERSIST>
-constexpr int min_waves() { return (PERSIST == 4 && P::E <= 16) ? 4 : 1; }
+constexpr int min_waves() {
+#ifdef VSIG_EXP_SPLIT_W4
+  return PERSIST == 4 ? 4 : 1;
+#else
+  return (PERSIST == 4 && P::E <= 16) ? 4 : 1;
+#endif
+}
 
 // Overlap-save kernels run one frame per block: TF threads (one wave for the
 // 1024 / 2048-point plans, whose barriers then cost nothing).

@@ -1,0 +1,146 @@
+// Streaming element-wise kernels on either side of the chain:
+//
+//   mix_c64          apply_frequency_shift (utils.py:120-127): x * exp(j*theta),
+//                    theta = (2*pi*f) * (i / sr) formed in double exactly as numpy
+//                    forms it, reduced mod 2*pi in double, sincos in fp32
+//   scale_c64        y = x * s (transplant_packet_in_vector's power scale,
+//                    utils.py:1481-1496)
+//   wv_quantize      SMU-WV int16 interleave of mat2wv
+//                    (vector_analyzer/mat_to_wv_converter.py:28-50)
+//   planar_to_c64    MAT v5 real / imaginary planes (any numeric storage type)
+//                    -> interleaved complex64 (load_packet, utils.py:48-86)
+//   c64_to_planar    complex64 -> float32 planes (save_vector, utils.py:659-670)
+//
+// All are HBM-bound grid-stride loops (8-16 B per element each way).
+#include <hip/hip_runtime.h>
+
+#include "vsig_kernels.h"
+
+namespace vsig {
+
+static int ew_grid(long long n) {
+  long long g = (n + 255) / 256;
+  if (g > 8192) g = 8192;
+  return g < 1 ? 1 : (int)g;
+}
+
+// ---------------------------------------------------------------- mixer
+__global__ __launch_bounds__(256) void mix_c64(const float2* __restrict__ x, long long n, double w,
+                                               double sr, long long i0, float2* __restrict__ y) {
+  // 2*pi split for a Cody-Waite reduction of theta = w * t (|theta| < 2^40 or so)
+  constexpr double kTwoPiHi = 6.28318530717958623200e+00;
+  constexpr double kTwoPiLo = 2.44929359829470635445e-16;
+  constexpr double kInvTwoPi = 1.59154943091895345608e-01;
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const double t = __ddiv_rn((double)(i0 + i), sr);   // np.arange(n) / sample_rate
+    const double th = __dmul_rn(w, t);                   // (2j*pi*f) * t, imaginary part
+    const double k = rint(th * kInvTwoPi);
+    const double r = fma(-k, kTwoPiLo, fma(-k, kTwoPiHi, th));
+    float s, c;
+    sincosf((float)r, &s, &c);
+    const float2 v = x[i];
+    y[i] = make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+  }
+}
+
+// ---------------------------------------------------------------- scale
+__global__ __launch_bounds__(256) void scale_c64(const float2* __restrict__ x, long long n, float s,
+                                                 float2* __restrict__ y) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const float2 v = x[i];
+    y[i] = make_float2(v.x * s, v.y * s);
+  }
+}
+
+// ---------------------------------------------------------------- SMU-WV
+// numpy's float32 -> int16 cast on x86: truncate to int32 (out of range and
+// NaN -> INT_MIN), keep the low 16 bits.
+__device__ __forceinline__ short np_f32_to_i16(float f) {
+  int v;
+  if (!(f > -2147483648.f && f < 2147483648.f)) v = (int)0x80000000u;
+  else v = (int)f;                                     // truncation toward zero
+  return (short)(v & 0xffff);
+}
+
+// norm > 0: signal / norm first, then * 32767 in float32, as mat2wv does.
+// numpy divides a complex64 by a real scalar with Smith's formula, which for
+// a zero imaginary divisor is a multiply by the rounded reciprocal 1/norm.
+__global__ __launch_bounds__(256) void wv_quantize(const float2* __restrict__ x, long long n, float norm,
+                                                   short2* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * 256;
+  const float rcp = norm > 0.f ? __fdiv_rn(1.f, norm) : 1.f;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    float2 v = x[i];
+    if (norm > 0.f) v = make_float2(v.x * rcp, v.y * rcp);
+    out[i] = make_short2(np_f32_to_i16(v.x * 32767.f), np_f32_to_i16(v.y * 32767.f));
+  }
+}
+
+// ---------------------------------------------------------------- MAT planes
+template <class T>
+__global__ __launch_bounds__(256) void planar_to_c64(const T* __restrict__ re, const T* __restrict__ im,
+                                                     long long n, float2* __restrict__ y) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+    y[i] = make_float2((float)re[i], im ? (float)im[i] : 0.f);
+}
+
+__global__ __launch_bounds__(256) void c64_to_planar(const float2* __restrict__ x, long long n,
+                                                     float* __restrict__ re, float* __restrict__ im) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+    const float2 v = x[i];
+    re[i] = v.x;
+    im[i] = v.y;
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_mix_c64(const float2* x, long long n, double w, double sr, long long i0, float2* y,
+                          hipStream_t st) {
+  hipLaunchKernelGGL(mix_c64, dim3(ew_grid(n)), dim3(256), 0, st, x, n, w, sr, i0, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale_c64(const float2* x, long long n, float s, float2* y, hipStream_t st) {
+  hipLaunchKernelGGL(scale_c64, dim3(ew_grid(n)), dim3(256), 0, st, x, n, s, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_wv_quantize(const float2* x, long long n, float norm, short* out, hipStream_t st) {
+  hipLaunchKernelGGL(wv_quantize, dim3(ew_grid(n)), dim3(256), 0, st, x, n, norm, (short2*)out);
+  return hipGetLastError();
+}
+
+// MAT v5 storage types (miINT8 = 1 ... miDOUBLE = 9)
+hipError_t launch_planar_to_c64(int mi_type, const void* re, const void* im, long long n, float2* y,
+                                hipStream_t st) {
+  const int g = ew_grid(n);
+#define VSIG_PLANES(T)                                                                          \
+  hipLaunchKernelGGL(planar_to_c64<T>, dim3(g), dim3(256), 0, st, (const T*)re, (const T*)im, n, y); \
+  break;
+  switch (mi_type) {
+    case 1: VSIG_PLANES(signed char)
+    case 2: VSIG_PLANES(unsigned char)
+    case 3: VSIG_PLANES(short)
+    case 4: VSIG_PLANES(unsigned short)
+    case 5: VSIG_PLANES(int)
+    case 6: VSIG_PLANES(unsigned int)
+    case 7: VSIG_PLANES(float)
+    case 9: VSIG_PLANES(double)
+    case 12: VSIG_PLANES(long long)
+    case 13: VSIG_PLANES(unsigned long long)
+    default: return hipErrorInvalidValue;
+  }
+#undef VSIG_PLANES
+  return hipGetLastError();
+}
+
+hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* im, hipStream_t st) {
+  hipLaunchKernelGGL(c64_to_planar, dim3(ew_grid(n)), dim3(256), 0, st, x, n, re, im);
+  return hipGetLastError();
+}
+
+}  // namespace vsig

@@ -630,6 +630,51 @@ int vsig_peak(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, vsig_peak_t*
   return VSIG_OK;
 }
 
+// ---------------------------------------------------------------- stream ops
+int vsig_mix_c64_dev(vsig_ctx* c, const void* x, int64_t n, double w, double sr, int64_t i0,
+                     void* y) {
+  if (!c || !x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 0 || !(sr != 0.0)) return fail(c, VSIG_E_INVALID, "need n >= 0 and sample_rate != 0");
+  if (n == 0) return VSIG_OK;
+  HIPCHK(c, vsig::launch_mix_c64((const float2*)x, n, w, sr, i0, (float2*)y, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_scale_c64_dev(vsig_ctx* c, const void* x, int64_t n, float s, void* y) {
+  if (!c || !x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 0) return fail(c, VSIG_E_INVALID, "n < 0");
+  if (n == 0) return VSIG_OK;
+  HIPCHK(c, vsig::launch_scale_c64((const float2*)x, n, s, (float2*)y, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_wv_quantize_dev(vsig_ctx* c, const void* x, int64_t n, float norm, int16_t* out) {
+  if (!c || !x || !out) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 0) return fail(c, VSIG_E_INVALID, "n < 0");
+  if (n == 0) return VSIG_OK;
+  HIPCHK(c, vsig::launch_wv_quantize((const float2*)x, n, norm, (short*)out, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_planar_to_c64_dev(vsig_ctx* c, int32_t mi_type, const void* re, const void* im, int64_t n,
+                           void* y) {
+  if (!c || !re || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 0) return fail(c, VSIG_E_INVALID, "n < 0");
+  if (n == 0) return VSIG_OK;
+  const hipError_t e = vsig::launch_planar_to_c64(mi_type, re, im, n, (float2*)y, c->stream);
+  if (e == hipErrorInvalidValue) return fail(c, VSIG_E_UNSUPPORTED, "MAT storage type");
+  HIPCHK(c, e);
+  return VSIG_OK;
+}
+
+int vsig_c64_to_planar_dev(vsig_ctx* c, const void* x, int64_t n, float* re, float* im) {
+  if (!c || !x || !re || !im) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 0) return fail(c, VSIG_E_INVALID, "n < 0");
+  if (n == 0) return VSIG_OK;
+  HIPCHK(c, vsig::launch_c64_to_planar((const float2*)x, n, re, im, c->stream));
+  return VSIG_OK;
+}
+
 // ---------------------------------------------------------------- PFB
 int vsig_pfb_c64_dev(vsig_ctx* c, const void* x, int64_t n, const float* h, int32_t ntaps,
                      int32_t nchan, void* y, int64_t nframes) {

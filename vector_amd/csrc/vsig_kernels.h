@@ -74,6 +74,15 @@ hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, i
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
                       float2* y, const float2* tw, int variant, int fpg, hipStream_t st);
 
+// stream_ops.hip
+hipError_t launch_mix_c64(const float2* x, long long n, double w, double sr, long long i0, float2* y,
+                          hipStream_t st);
+hipError_t launch_scale_c64(const float2* x, long long n, float s, float2* y, hipStream_t st);
+hipError_t launch_wv_quantize(const float2* x, long long n, float norm, short* out, hipStream_t st);
+hipError_t launch_planar_to_c64(int mi_type, const void* re, const void* im, long long n, float2* y,
+                                hipStream_t st);
+hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* im, hipStream_t st);
+
 // analysis.hip
 hipError_t launch_radix_hist(int dtype, const void* a, long long n, const unsigned long long* prefix,
                              const unsigned long long* mask, int nq, int shift,
