@@ -34,6 +34,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Msamples/s c64 through FIR+FFT+xcorr chain; 1/2/4/8 GPU + %HBM roofline"
 HBM_PEAK_GBS = 8000.0          # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+FP32_PEAK_TF = 157.3           # MI355X FP32 vector peak (packed FMA), MI355X_MICROARCH.md
 TONES = ((1.0, 0.05), (0.5, 0.11), (0.25, -0.20))
 
 
@@ -90,6 +91,14 @@ def cpu_baseline(samples, taps, nfft, tmpl):
                         f"np.correlate complex128 L={len(tmpl)} valid + find_correlation_peak; "
                         f"{dt:.2f} s, 1 thread"),
                 seconds=round(dt, 3))
+
+
+def xcorr_block(L, forced):
+    """Overlap-save block size the correlator plans for a template of L
+    (vsig_api.hip os_size_xcorr, unless forced with --xcorr-m)."""
+    if forced:
+        return forced
+    return 4096 if L <= 1024 else 8192 if L <= 2048 else 16384
 
 
 def load_traffic(key):
@@ -224,6 +233,29 @@ def main():
                 "algorithmic_bytes": bytes_per_launch[dom],
                 "avg_launch_ms": round(stages[dom], 4),
                 "traffic_source": pmc["source"] if pmc else None}
+    # every stage against its own roof: HBM bytes for all three, and for the
+    # correlator (not HBM-bound) the FP32 vector roof with the standard
+    # 5 N log2 N FFT flop count (2 FFTs + the spectrum multiply per block)
+    stage_roof = {}
+    for k, ms in stages.items():
+        gbs = bytes_per_launch[k] / (ms * 1e-3) / 1e9
+        stage_roof[k] = {"ms": round(ms, 4), "bytes": bytes_per_launch[k], "GBs": round(gbs, 1),
+                         "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+    if "xcorr" in stages:
+        M = xcorr_block(args.template, args.xcorr_m)
+        L = args.template
+        hop = M - L + 1
+        nb = -(-(ny + chain.yhalo - L + 1) // hop)
+        flops = nb * (2 * 5 * M * np.log2(M) + 6 * M)
+        tf = flops / (stages["xcorr"] * 1e-3) / 1e12
+        stage_roof["xcorr"].update({"flops": int(flops), "TFLOPs": round(tf, 2),
+                                    "valu_peak_TFLOPs": FP32_PEAK_TF,
+                                    "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
+    if "fir" in stages and "psd" in stages:
+        b = bytes_per_launch["fir"] + bytes_per_launch["psd"]
+        t = (stages["fir"] + stages["psd"]) * 1e-3
+        stage_roof["fir+psd"] = {"GBs": round(b / t / 1e9, 1),
+                                 "hbm_frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_samples, taps, args.nfft, tmpl)
@@ -244,6 +276,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "stages_roofline": stage_roof,
         "check": check,
     }
     print(json.dumps(out), flush=True)

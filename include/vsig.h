@@ -88,6 +88,10 @@ int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 /* Tuning micro-benchmark: `iters` in-LDS FFTs on each of `frames` frames of
  * the plan `key` (4096 / 8192 / 16384, -1024 / -2048 / -16384 for the
  * overlap-save one-wave and 512-thread plans); io: frames * |key| complex64. */
+/* HBM ceiling probe for the tuning tools: copy n complex64 x -> y with
+ * variant 0: 8-B lanes, 1: 8-B + non-temporal stores, 2: 16-B lanes,
+ * 3: 16-B + non-temporal stores; grid 0 = default. */
+int vsig_copy_bench(vsig_ctx* ctx, const void* x, int64_t n, void* y, int variant, int grid);
 int vsig_fft_bench(vsig_ctx* ctx, int key, void* io, int frames, int iters, int twl);
 /* Per-kernel timing with HIP events on the context stream (for bench.py):
  * enable, run, then read the mean duration in ms of each kernel family. */

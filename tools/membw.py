@@ -1,10 +1,18 @@
-"""Practical HBM ceilings on this box: device copy (read+write) and a read-only
-reduction over 2**28 complex64 (2 GiB), timed with HIP events."""
+"""Practical HBM ceilings on this box: torch copy, and libvsig's copy probe with
+8-B / 16-B lanes and plain / non-temporal stores over 2**28 complex64 (2 GiB
+read + 2 GiB written), timed with HIP events; plus a read-only reduction."""
 import json
+import os
+import sys
+
 import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 n = 1 << 28
 x = torch.randn(n, dtype=torch.complex64, device="cuda")
 y = torch.empty_like(x)
+
+
 def t(fn, it=20):
     fn(); torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -13,8 +21,20 @@ def t(fn, it=20):
         fn()
     e1.record(); torch.cuda.synchronize()
     return e0.elapsed_time(e1) / it
+
+
+res = {}
 ms = t(lambda: y.copy_(x))
+res["torch_copy"] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
 xr = torch.view_as_real(x)
-ms2 = t(lambda: xr.sum())
-print(json.dumps({"copy_ms": round(ms, 4), "copy_GBs": round(2 * 8 * n / ms / 1e6, 1),
-                  "read_ms": round(ms2, 4), "read_GBs": round(8 * n / ms2 / 1e6, 1)}))
+ms = t(lambda: xr.sum())
+res["torch_read_sum"] = (round(ms, 4), round(8 * n / ms / 1e6, 1))
+import vector_amd as va
+from vector_amd import dsp
+ctx = va.get_context(0)
+ctx.bind_stream()
+for v, name in ((0, "probe_8B"), (1, "probe_8B_nt"), (2, "probe_16B"), (3, "probe_16B_nt")):
+    for grid in (0, 2048, 16384):
+        ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, grid), "c"))
+        res[f"{name}_g{grid}"] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
+print(json.dumps(res))

@@ -144,3 +144,46 @@ hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* 
 }
 
 }  // namespace vsig
+
+namespace vsig {
+// ---------------------------------------------------------------- copy probe
+// HBM ceiling probe for the tuning tools (tools/membw.py): copy n complex64
+// with 8-B (float2) or 16-B (float4) lanes, plain or non-temporal stores.
+template <int W, bool NT>
+__global__ __launch_bounds__(256) void copy_probe(const float2* __restrict__ x, long long n,
+                                                  float2* __restrict__ y) {
+  const long long stride = (long long)gridDim.x * 256;
+  typedef float v4 __attribute__((ext_vector_type(4)));
+  typedef float v2 __attribute__((ext_vector_type(2)));
+  if constexpr (W == 16) {
+    const v4* x4 = reinterpret_cast<const v4*>(x);
+    v4* y4 = reinterpret_cast<v4*>(y);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n / 2; i += stride) {
+      const v4 v = x4[i];
+      if constexpr (NT) __builtin_nontemporal_store(v, y4 + i);
+      else y4[i] = v;
+    }
+  } else {
+    const v2* x2 = reinterpret_cast<const v2*>(x);
+    v2* y2 = reinterpret_cast<v2*>(y);
+    for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
+      const v2 v = x2[i];
+      if constexpr (NT) __builtin_nontemporal_store(v, y2 + i);
+      else y2[i] = v;
+    }
+  }
+}
+
+hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
+                             hipStream_t st) {
+  const dim3 g(grid > 0 ? grid : 8192), b(256);
+  switch (variant) {
+    case 0: hipLaunchKernelGGL((copy_probe<8, false>), g, b, 0, st, x, n, y); break;
+    case 1: hipLaunchKernelGGL((copy_probe<8, true>), g, b, 0, st, x, n, y); break;
+    case 2: hipLaunchKernelGGL((copy_probe<16, false>), g, b, 0, st, x, n, y); break;
+    case 3: hipLaunchKernelGGL((copy_probe<16, true>), g, b, 0, st, x, n, y); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+}  // namespace vsig

@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{16, 8, 10};         // tuned defaults (see vsig_set_option)
+  vsig::Variants var{16, 8, 2};          // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
   int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
@@ -350,6 +350,13 @@ int vsig_fft_bench(vsig_ctx* c, int key, void* io, int frames, int iters, int tw
   if (rc) return rc;
   Timed t(c, "fft_bench");
   HIPCHK(c, vsig::launch_fft_bench(key, (float2*)io, frames, iters, tw, twl, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_copy_bench(vsig_ctx* c, const void* x, int64_t n, void* y, int variant, int grid) {
+  if (!c || !x || !y || n < 0) return fail(c, VSIG_E_INVALID, "bad arguments");
+  Timed t(c, "copy_bench");
+  HIPCHK(c, vsig::launch_copy_probe((const float2*)x, n, (float2*)y, variant, grid, c->stream));
   return VSIG_OK;
 }
 

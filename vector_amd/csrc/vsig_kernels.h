@@ -82,6 +82,8 @@ hipError_t launch_wv_quantize(const float2* x, long long n, float norm, short* o
 hipError_t launch_planar_to_c64(int mi_type, const void* re, const void* im, long long n, float2* y,
                                 hipStream_t st);
 hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* im, hipStream_t st);
+hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
+                             hipStream_t st);
 
 // analysis.hip
 hipError_t launch_radix_hist(int dtype, const void* a, long long n, const unsigned long long* prefix,
