@@ -42,15 +42,16 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def design(ntaps, L):
+def design(ntaps, L, decim=1):
     import scipy.signal
     taps = scipy.signal.firwin(ntaps, 0.2).astype(np.float32)
     rng = np.random.default_rng(4096)
-    b = rng.integers(0, 2, size=(2, L))
+    b = rng.integers(0, 2, size=(2, L * decim))
     pre = (((2 * b[0] - 1) + 1j * (2 * b[1] - 1)) / np.sqrt(2)).astype(np.complex64)
-    # The template is the preamble as it leaves the receive filter (causal part),
-    # so the filtered capture contains it exactly at the planted offset.
-    tmpl = np.convolve(pre, taps)[:L].astype(np.complex64)
+    # The template is the preamble as it leaves the receive filter and the
+    # decimator (causal part, every decim-th sample): the filtered, decimated
+    # capture contains it exactly at the planted offset / decim.
+    tmpl = np.convolve(pre, taps)[:L * decim][::decim].astype(np.complex64)
     return taps, pre, tmpl
 
 
@@ -158,7 +159,7 @@ def main():
     from vector_amd.shard import ChainConfig, HipBackend, StreamChain
 
     n = args.samples
-    taps, pre, tmpl = design(args.ntaps, args.template)
+    taps, pre, tmpl = design(args.ntaps, args.template, args.decim)
     from vector_amd._lib import get_context
     ctx0 = get_context(local)
     for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m"):

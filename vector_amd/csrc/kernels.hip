@@ -275,11 +275,15 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
       if (i >= 0 && i < lim) yb[(unsigned)i] = cconj(v[e]);
     }
   } else {
+    // i / decim by a multiply-high with m = floor(2^32 / decim) + 1: exact for
+    // i, decim < 2^16 (hop <= 16384), no per-element integer division
     float2* yb = y + gb / decim;
+    const unsigned mg = 0xffffffffu / (unsigned)decim + 1u;
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e) - lo;
-      if (i >= 0 && i < lim && i % decim == 0) yb[(unsigned)(i / decim)] = cconj(v[e]);
+      const unsigned q = __umulhi((unsigned)i, mg);
+      if (i >= 0 && i < lim && (unsigned)i == q * (unsigned)decim) yb[q] = cconj(v[e]);
     }
   }
 }
