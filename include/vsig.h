@@ -81,10 +81,14 @@ int vsig_set_stream(vsig_ctx* ctx, void* hip_stream);
 int vsig_synchronize(vsig_ctx* ctx);
 /* Tuning knobs (defaults are the measured best on MI355X):
  *   "psd_variant" / "fir_variant" / "xcorr_variant": bit 0 persistent kernel
- *   (next-unit prefetch, register twiddles), bit 1 (M = 16384) 512-thread plan;
+ *   (next-unit prefetch, register twiddles), bit 1 (M = 16384) 512-thread plan,
+ *   bit 3 LDS twiddles, bit 4 split re/im exchange, bit 5 (xcorr) partitioned
+ *   template, bit 6 (xcorr, M = 16384) half-frame kernel (two blocks per CU);
  *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule.
  * Plans created afterwards use the new block sizes. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
+/* Current value of a tuning knob (same keys as vsig_set_option). */
+int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
 /* Tuning micro-benchmark: `iters` in-LDS FFTs on each of `frames` frames of
  * the plan `key` (4096 / 8192 / 16384, -1024 / -2048 / -16384 for the
  * overlap-save one-wave and 512-thread plans); io: frames * |key| complex64. */

@@ -10,11 +10,13 @@ from oracle import ref
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("decim,pipeline", [(1, 1), (4, 1), (2, 4)])
-def test_stream_chain_matches_oracle(gpu, decim, pipeline):
+@pytest.mark.parametrize("decim,pipeline,L", [(1, 1, 512), (4, 1, 512), (2, 4, 512), (1, 1, 4096),
+                                              (4, 1, 4096)])
+def test_stream_chain_matches_oracle(gpu, decim, pipeline, L):
+    """L = 4096 runs the bench's correlator (M = 16384, half-frame kernel)."""
     import torch
     from vector_amd.shard import ChainConfig, HipBackend, StreamChain
-    n, L, nfft = 1 << 20, 512, 1024
+    n, nfft = 1 << 20, 1024
     taps = scipy.signal.firwin(255, 0.2).astype(np.float32)
     rng = np.random.default_rng(decim)
     b = rng.integers(0, 2, size=(2, L * decim))

@@ -7,6 +7,7 @@ float32 spectra within 1e-5 relative, measured per frame against the frame's
 maximum (SURVEY.md §7 hard part (v)); FIR and correlation outputs within 1e-5
 of max |reference| (norm-wise: fp32 FFT vs direct-sum numpy / complex128).
 """
+import ctypes as C
 import glob
 import os
 
@@ -287,7 +288,7 @@ def test_correlator_stream_full_size_property(gpu):
     assert peak == pytest.approx(direct, rel=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40, 64, 65, 72])
 def test_kernel_variants_agree_with_oracle(gpu, variant):
     """Every tuning variant (persistent / LDS twiddles / split exchange /
     512-thread 16k plan) must give the same results as the oracle."""
@@ -296,6 +297,12 @@ def test_kernel_variants_agree_with_oracle(gpu, variant):
     x = ref.synth_iq(3 * 16384 + 77, seed=variant)
     taps = rng.standard_normal(255).astype(np.float32)
     tmpl = ref.qpsk_preamble(4096, seed=variant)
+    keys = ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m")
+    saved = {}
+    for k in keys:
+        v = C.c_int()
+        ctx.check(ctx.lib.vsig_get_option(ctx.h, k.encode(), C.byref(v)), k)
+        saved[k] = v.value
     try:
         for k in ("psd_variant", "fir_variant", "xcorr_variant"):
             ctx.check(ctx.lib.vsig_set_option(ctx.h, k.encode(), variant), k)
@@ -330,10 +337,6 @@ def test_kernel_variants_agree_with_oracle(gpu, variant):
                 assert peak == pytest.approx(a.max(), rel=1e-5)
                 assert s1 == pytest.approx(a.sum(), rel=1e-5)
     finally:
-        lib, h = ctx.lib, ctx.h
-        lib.vsig_set_option(h, b"psd_variant", 8)
-        lib.vsig_set_option(h, b"fir_variant", 8)
-        lib.vsig_set_option(h, b"xcorr_variant", 10)
-        lib.vsig_set_option(h, b"fir_m", 0)
-        lib.vsig_set_option(h, b"xcorr_m", 0)
+        for k, v in saved.items():
+            ctx.lib.vsig_set_option(ctx.h, k.encode(), v)
         gpu.dsp._fir_cache.clear()

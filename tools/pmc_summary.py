@@ -17,7 +17,7 @@ import sys
 from collections import defaultdict
 
 FAMILY = {"fir_os_kernel": "fir", "psd_kernel": "psd", "xcorr_os_kernel": "xcorr",
-          "xcorr_part_kernel": "xcorr", "pfb_kernel": "pfb",
+          "xcorr_part_kernel": "xcorr", "xcorr_half_kernel": "xcorr", "pfb_kernel": "pfb",
           "peak_reduce": "peak", "partial_finalize": "finalize"}
 
 

@@ -3,7 +3,7 @@ import re
 import subprocess
 import sys
 
-src = sys.argv[1] if len(sys.argv) > 1 else "vector_amd/csrc/kernels.hip"
+src = sys.argv[1] if len(sys.argv) > 1 else "vector_amd/csrc/xcorr.hip"
 flt = sys.argv[2] if len(sys.argv) > 2 else ""
 out = subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-c", src,
                       "-o", "/tmp/_regs.o", "-Rpass-analysis=kernel-resource-usage"],

@@ -45,6 +45,7 @@ SIGNATURES = {
     "vsig_set_stream": (C.c_int, [P, P]),
     "vsig_synchronize": (C.c_int, [P]),
     "vsig_set_option": (C.c_int, [P, C.c_char_p, C.c_int]),
+    "vsig_get_option": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
     "vsig_copy_bench": (C.c_int, [P, P, I64, P, C.c_int, C.c_int]),
     "vsig_fft_bench": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_int]),
     "vsig_timing_enable": (C.c_int, [P, C.c_int]),

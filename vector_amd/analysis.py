@@ -7,7 +7,7 @@ rows a3, a7, a8):
 
 The data-parallel work — |S| order statistics, the dB transform, the |x|^2
 prefix scan and boxcar smoothing, the threshold scan, the magnitude
-correlation — runs in libvsig.so (analysis.hip, kernels.hip).  What is left on
+correlation — runs in libvsig.so (analysis.hip, psd.hip, xcorr.hip, reduce.hip).  What is left on
 the host is O(1) scalar arithmetic, written so that numpy's own rules
 (np.percentile 'linear' in the array's dtype, np.median, NEP 50 promotion)
 give the same numbers the reference computes.

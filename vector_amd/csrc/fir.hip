@@ -1,0 +1,157 @@
+// Overlap-save FIR kernel (gfx950), decimation folded into the store (filter).
+#include "os_common.hpp"
+
+namespace vsig {
+
+// Store the valid outputs of FIR block b (conj undoes the inverse-by-conj
+// trick): block-local 32-bit offsets from a per-block base; hop is a multiple
+// of decim, so the decimation phase is the local index's.
+template <class P>
+__device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ y, long long b,
+                                          long long hop, int lo, long long nloc, int decim, int t) {
+  const long long gb = b * hop;
+  const long long rem = nloc - gb;
+  const int lim = rem < hop ? (int)rem : (int)hop;
+  if (decim == 1) {
+    float2* yb = y + gb;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e) - lo;
+      if (i >= 0 && i < lim) yb[(unsigned)i] = cconj(v[e]);
+    }
+  } else {
+    // i / decim by a multiply-high with m = floor(2^32 / decim) + 1: exact for
+    // i, decim < 2^16 (hop <= 16384), no per-element integer division
+    float2* yb = y + gb / decim;
+    const unsigned mg = 0xffffffffu / (unsigned)decim + 1u;
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e) - lo;
+      const unsigned q = __umulhi((unsigned)i, mg);
+      if (i >= 0 && i < lim && (unsigned)i == q * (unsigned)decim) yb[q] = cconj(v[e]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// FIR, overlap-save.  Block b produces outputs g in [b*hop, b*hop + hop) of
+//   y[g] = sum_{m < ntaps} h[m] x[g0 + g - m]   (x = 0 outside [0, n))
+// i.e. np.convolve(x, h, 'full')[g0:n]; only g % decim == 0 is stored, at
+// g/decim.  The first g0 samples are history (a time-chunk's left halo).
+// The segment x[b*hop - (ntaps-1) .. + M) is FFT'd, multiplied by Hs = FFT(h)/M
+// and inverse-transformed (conj trick), all in LDS / registers.
+// ---------------------------------------------------------------------------
+template <class P, int PERSIST>
+__global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fir_os_kernel(
+    const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
+    int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
+    const float2* __restrict__ tw) {
+  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+  constexpr int BT = os_threads<P>();
+  static_assert(BT == P::TF, "one frame per block");
+  __shared__ float2 lds[os_lds<P, PERSIST>()];
+  const int t = threadIdx.x;
+  long long b = PERSIST == 0 || PERSIST >= 3 ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  if (b >= nblocks) return;  // uniform per block
+
+  const int lo = ntaps - 1;
+  const long long nloc = n - g0;
+  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
+    float2* t2 = lds + (P::LDS + 1) / 2;
+    float* ldf = reinterpret_cast<float*>(lds);
+    load_tw2<P>(t2, tw, t, BT);
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame_split<P>(v, ldf, t2, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame_split<P>(v, ldf, t2, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  }
+  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
+    float2* t2 = lds + P::LDS;
+    load_tw2<P>(t2, tw, t, BT);
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame_t2<P>(v, lds, t2, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame_t2<P>(v, lds, t2, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  }
+  if constexpr (!PERSIST) {          // one unit per block, table twiddles
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame<P>(v, lds, tw, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    for (; b < nblocks; b += gridDim.x) {
+      fft_frame<P>(v, lds, tw, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+      float2 nv[P::E];
+      const long long nb = b + gridDim.x;
+      fft_frame_hook<P>(v, lds, tw, t, [&] {
+        if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
+      });
+      fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
+    }
+    return;
+  }
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 v[P::E];
+  load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+  for (; b < nblocks; b += gridDim.x) {
+    fft_frame_anch<P>(v, lds, wa, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    // Prefetch after the (L2-resident) filter-spectrum loads: vmcnt retires in
+    // issue order, so the next segment then lands behind the inverse FFT.
+    float2 nv[P::E];
+    const long long nb = b + gridDim.x;
+    if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
+    fft_frame_anch<P>(v, lds, wa, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = nv[e];
+  }
+}
+
+template <class PL, int PERSIST>
+void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, int ntaps,
+                  long long hop, int decim, float2* y, long long nblocks, const float2* tw,
+                  hipStream_t st) {
+  const long long grid =
+      (PERSIST == 1 || PERSIST == 2)
+          ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks) : nblocks;
+  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(os_threads<PL>()),
+                     0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
+}
+
+hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
+                         int ntaps, long long hop, int decim, float2* y, const float2* tw,
+                         int variant, hipStream_t st) {
+  if (n - g0 <= 0) return hipSuccess;
+  const long long nblocks = (n - g0 + hop - 1) / hop;
+  VSIG_OS_SWITCH(M, variant, {
+    if (variant & 16) launch_fir_t<PL, 4>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 4) launch_fir_t<PL, 2>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else launch_fir_t<PL, 0>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+  });
+  return hipGetLastError();
+}
+
+}  // namespace vsig

@@ -1,0 +1,184 @@
+// Shared pieces of the overlap-save / streaming kernels (gfx950): launch
+// geometry, segment loads, DPP wave reductions of |c| partials, plan switches.
+// Included by psd.hip, fir.hip, xcorr.hip, reduce.hip (one translation unit
+// each, compiled in parallel; every kernel is launched from its own TU).
+#pragma once
+#include "fft_engine.hpp"
+#include "vsig_kernels.h"
+
+namespace vsig {
+// Occupancy request (min waves per SIMD) of a kernel variant: the split
+// exchange (variant 4) exists to fit two 16k / four 8k frames per CU, which
+// needs <= 128 VGPRs, so ask the register allocator for 4 waves/SIMD there.
+template <class P, int PERSIST>
+constexpr int min_waves() {
+#ifdef VSIG_EXP_SPLIT_W4
+  return PERSIST == 4 ? 4 : 1;
+#else
+  return (PERSIST == 4 && P::E <= 16) ? 4 : 1;
+#endif
+}
+
+// Overlap-save kernels run one frame per block: TF threads (one wave for the
+// 1024 / 2048-point plans, whose barriers then cost nothing).
+template <class P>
+constexpr int os_threads() { return P::TF; }
+
+// LDS (in float2) of a one-frame block: data (halved by the split exchange)
+// plus the two-level twiddle table for variants 3 and 4.
+template <class P, int PERSIST>
+constexpr int os_lds() {
+  return (PERSIST == 4 ? (P::LDS + 1) / 2 : P::LDS) +
+         ((PERSIST == 3 || PERSIST == 4) ? tw2_size<P>() : 0);
+}
+
+// Pass-0 operands of an overlap-save segment x[s0 .. s0 + N) with zero fill
+// outside [0, n).  The block-uniform base keeps the address in SGPRs; interior
+// segments (the common case) skip the per-element bounds test.
+template <class P>
+__device__ __forceinline__ void load_segment(float2* v, const float2* __restrict__ x,
+                                             long long s0, long long n, int t) {
+  const float2* base = x + s0;
+  if (s0 >= 0 && s0 + P::N <= n) {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = base[(unsigned)in_index<P>(t, e)];
+  } else {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = in_index<P>(t, e);
+      const long long xi = s0 + i;
+      v[e] = (xi >= 0 && xi < n) ? base[i] : make_float2(0.f, 0.f);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Block partial of a |c| reduction: max |c|^2 (lowest index on ties),
+// sum |c|, sum |c|^2.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void better(float& m, long long& i, float m2, long long i2) {
+  if (m2 > m || (m2 == m && i2 < i)) { m = m2; i = i2; }
+}
+__device__ __forceinline__ void betterd(double& m, long long& i, double m2, long long i2) {
+  if (m2 > m || (m2 == m && i2 < i)) { m = m2; i = i2; }
+}
+
+template <int BT>
+__device__ __forceinline__ void block_partial(double m, long long mi, double s1, double s2,
+                                              PeakPartial* out) {
+  // wave reduce (64 lanes)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double om = __shfl_xor(m, off);
+    const long long oi = __shfl_xor(mi, off);
+    betterd(m, mi, om, oi);
+    s1 += __shfl_xor(s1, off);
+    s2 += __shfl_xor(s2, off);
+  }
+  constexpr int NW = BT / 64;
+  __shared__ double sm[NW], ss1[NW], ss2[NW];
+  __shared__ long long si[NW];
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  if (l == 0) { sm[w] = m; si[w] = mi; ss1[w] = s1; ss2[w] = s2; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int q = 1; q < NW; ++q) { betterd(m, mi, sm[q], si[q]); s1 += ss1[q]; s2 += ss2[q]; }
+    out->max2 = m; out->idx = mi; out->sum_abs = s1; out->sum_abs2 = s2;
+  }
+}
+
+// Partials of the correlators: float |c|^2 / int block-local index / float
+// sums, wave-reduced with DPP (VALU-rate lane moves instead of a chain of
+// ds_bpermute round trips and a block barrier — a block's tail is exposed at
+// one block per CU), one partial per wave.  rev: ties go to the larger index.
+template <int CTRL, int RM>
+__device__ __forceinline__ float dpp_f(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, RM, 0xf, false));
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ int dpp_i(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ void peak_dpp_step(float& m, int& mi, float& s1, float& s2, bool rev) {
+  const float om = dpp_f<CTRL, RM>(m);
+  const int oi = dpp_i<CTRL, RM>(mi);
+  const bool take = (om > m) | ((om == m) & (rev ? oi > mi : oi < mi));
+  m = take ? om : m;
+  mi = take ? oi : mi;
+  s1 += dpp_f<CTRL, RM>(s1);
+  s2 += dpp_f<CTRL, RM>(s2);
+}
+
+// One partial per wave (no block barrier at the block's tail): lane 63 holds
+// the wave's result after the DPP steps and writes it.
+__device__ __forceinline__ void wave_partial_f(float m, int mi, float s1, float s2, bool rev,
+                                               long long ob, long long nout, PeakPartial* out) {
+  // rocPRIM-style wave64 reduction: quad xor 1, 2; row_ror 4, 8; row_bcast 15, 31
+  // -> lane 63 holds the wave's result (rows not feeding it hold garbage).
+  peak_dpp_step<0xb1, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x4e, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x124, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x128, 0xf>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x142, 0xa>(m, mi, s1, s2, rev);
+  peak_dpp_step<0x143, 0xc>(m, mi, s1, s2, rev);
+  if ((threadIdx.x & 63) == 63) {
+    long long gi = ob + mi;
+    if (rev) gi = nout - 1 - gi;
+    PeakPartial r;
+    r.max2 = (double)m;
+    r.idx = gi;
+    r.sum_abs = (double)s1;
+    r.sum_abs2 = (double)s2;
+    *out = r;
+  }
+}
+
+// Resident blocks of a persistent kernel: CUs x blocks per CU (occupancy API).
+template <class K>
+long long persistent_grid(K kernel, int block, long long units) {
+  static thread_local int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (cus <= 0) cus = 256;
+  }
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, block, 0) != hipSuccess || per < 1)
+    per = 1;
+  const long long g = (long long)cus * per;
+  return units < g ? units : g;
+}
+
+#define VSIG_PLAN_SWITCH(N, ...)                          \
+  switch (N) {                                             \
+    case 64: { using PL = Plan64; __VA_ARGS__; } break;           \
+    case 128: { using PL = Plan128; __VA_ARGS__; } break;         \
+    case 256: { using PL = Plan256; __VA_ARGS__; } break;         \
+    case 512: { using PL = Plan512; __VA_ARGS__; } break;         \
+    case 1024: { using PL = Plan1024; __VA_ARGS__; } break;       \
+    case 2048: { using PL = Plan2048; __VA_ARGS__; } break;       \
+    case 4096: { using PL = Plan4096; __VA_ARGS__; } break;       \
+    case 8192: { using PL = Plan8192; __VA_ARGS__; } break;       \
+    case 16384: { using PL = Plan16384; __VA_ARGS__; } break;     \
+    default: return hipErrorInvalidValue;                  \
+  }
+
+// Only plans with one frame per block can run the overlap-save kernels.
+// variant bit 0: persistent (prefetch + register anchors); bit 1: the E = 32 /
+// 512-thread plan for M = 16384 instead of E = 16 / 1024 threads.
+#define VSIG_OS_SWITCH(N, V, ...)                                          \
+  switch (N) {                                                              \
+    case 1024: { using PL = Plan1024s; __VA_ARGS__; } break;                \
+    case 2048: { using PL = Plan2048s; __VA_ARGS__; } break;                \
+    case 4096: { using PL = Plan4096; __VA_ARGS__; } break;                        \
+    case 8192: { using PL = Plan8192; __VA_ARGS__; } break;                        \
+    case 16384:                                                             \
+      if ((V) & 2) { using PL = Plan16384w; __VA_ARGS__; }                         \
+      else { using PL = Plan16384; __VA_ARGS__; }                                  \
+      break;                                                                \
+    default: return hipErrorInvalidValue;                                   \
+  }
+
+}  // namespace vsig

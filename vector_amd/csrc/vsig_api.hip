@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{16, 8, 2};          // tuned defaults (see vsig_set_option)
+  vsig::Variants var{16, 8, 65};         // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
   int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
@@ -95,6 +95,7 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
 // Twiddle-table key of the plan an overlap-save launch of size M uses.
 int tw_key(int M, int variant) {
   if (M == 1024 || M == 2048) return -M;           // one-wave plans
+  if (M == 16384 && (variant & 64)) return 8192;   // half-frame correlator: 8192-point plan
   return (M == 16384 && (variant & 2)) ? -16384 : M;
 }
 
@@ -128,7 +129,26 @@ int get_tw2(vsig_ctx* c, int N, const float2** out) {
 // two-level table.  os: an overlap-save launch (its own plans for 1k / 2k / 16k).
 int get_tw_for(vsig_ctx* c, int M, int variant, bool os, const float2** out) {
   const int key = os ? tw_key(M, variant) : M;
-  return (variant & 24) ? get_tw2(c, key, out) : get_twiddles(c, key, out);
+  return (variant & 24) ? get_tw2(c, key, out) : get_twiddles(c, key, out);   // anchors: per-pass table
+}
+
+// W_M^t for t < T (the per-thread twiddle of the half-frame correlator),
+// cached under key M + 2^21.
+int get_half_tw(vsig_ctx* c, int M, int T, const float2** out) {
+  const int key = M + (1 << 21);
+  auto it = c->tw.find(key);
+  if (it != c->tw.end()) { *out = it->second; return VSIG_OK; }
+  std::vector<float2> h;
+  for (int t = 0; t < T; ++t) {
+    const double a = -2.0 * M_PI * (double)t / (double)M;
+    h.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+  }
+  float2* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, h.size() * sizeof(float2)));
+  HIPCHK(c, hipMemcpy(d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice));
+  c->tw[key] = d;
+  *out = d;
+  return VSIG_OK;
 }
 
 int ensure_partials(vsig_ctx* c, long long n) {
@@ -243,6 +263,11 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, co
   const float2* tw;
   rc = get_tw_for(c, M, var, true, &tw);
   if (rc) return rc;
+  const float2* wt = nullptr;
+  if (!Ps1 && M == 16384 && (var & 64)) {
+    rc = get_half_tw(c, M, 256, &wt);
+    if (rc) return rc;
+  }
   {
     Timed t(c, "xcorr");
     if (Ps1)
@@ -250,7 +275,7 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, co
                                         c->partials, tw, (var & 8) ? 1 : 0, c->stream));
     else
       HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
-                                      c->partials, tw, c->var.xcorr, c->stream));
+                                      c->partials, tw, wt, c->var.xcorr, c->stream));
   }
   return finalize_peak(c, nparts, 1, peak_dev);
 }
@@ -326,7 +351,7 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   const std::string k(key);
   if (k == "psd_variant") c->var.psd = value & 29;
   else if (k == "fir_variant") c->var.fir = value & 31;
-  else if (k == "xcorr_variant") c->var.xcorr = value & 63;
+  else if (k == "xcorr_variant") c->var.xcorr = value & 127;
   else if (k == "fir_m" || k == "xcorr_m") {
     if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
         value != 16384)
@@ -340,6 +365,20 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }
+  return VSIG_OK;
+}
+
+int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
+  if (!c || !key || !value) return VSIG_E_INVALID;
+  const std::string k(key);
+  if (k == "psd_variant") *value = c->var.psd;
+  else if (k == "fir_variant") *value = c->var.fir;
+  else if (k == "xcorr_variant") *value = c->var.xcorr;
+  else if (k == "fir_m") *value = c->fir_m;
+  else if (k == "xcorr_m") *value = c->xcorr_m;
+  else if (k == "pfb_variant") *value = c->pfb_variant;
+  else if (k == "pfb_fpg") *value = c->pfb_fpg;
+  else return VSIG_E_INVALID;
   return VSIG_OK;
 }
 

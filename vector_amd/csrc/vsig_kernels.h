@@ -40,7 +40,9 @@ hipError_t tw2_info(int N, int* shift, int* hi);
 // Kernel variants (tuning): bit 0 persistent + register twiddle anchors;
 // bit 1 (M = 16384) E = 32 plan; bit 2 persistent + late prefetch; bit 3
 // two-level LDS twiddle table (one unit per block); bit 4 split re/im LDS
-// exchange; bit 5 (xcorr) partitioned correlation with M = L-point FFTs.
+// exchange; bit 5 (xcorr) partitioned correlation with M = L-point FFTs;
+// bit 6 (xcorr, M = 16384) half-frame kernel: two 8192-point halves through
+// LDS, two blocks per CU (wt = W_M^t table, t < 256).
 struct Variants { int psd, fir, xcorr; };
 
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
@@ -53,8 +55,8 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
                          int variant, hipStream_t st);
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
-                           PeakPartial* partials, const float2* tw, int variant,
-                           hipStream_t st);
+                           PeakPartial* partials, const float2* tw, const float2* wt,
+                           int variant, hipStream_t st);
 // Partitioned correlation (template halves P0 / P1 of Lp = M / 2 samples).
 hipError_t launch_xcorr_part(int M, const float2* s, long long n, const float2* P0,
                              const float2* P1, long long off, long long nout, float2* c,
