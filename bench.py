@@ -132,6 +132,8 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="sub-chunks per step: FIR / PSD / xcorr overlap on three HIP streams")
+    ap.add_argument("--serial", action="store_true",
+                    help="run the --pipeline sub-chunks in order on one stream (cache reuse)")
     for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m"):
         ap.add_argument("--" + k.replace("_", "-"), type=int, default=None)
     ap.add_argument("--workload", choices=("chain", "pfb"), default="chain",
@@ -167,7 +169,7 @@ def main():
         if v is not None:
             ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, k.encode(), v), k)
     cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl,
-                      pipeline=args.pipeline)
+                      pipeline=args.pipeline, serial=args.serial)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)
     N = world * n
@@ -273,7 +275,7 @@ def main():
                    "samples_per_gpu": n, "total_samples": N, "ntaps": args.ntaps,
                    "decim": args.decim, "nfft": args.nfft, "template": args.template,
                    "parallelism": f"time-chunk x{world} (RCCL halos)",
-                   "pipeline": args.pipeline},
+                   "pipeline": args.pipeline, "serial": args.serial},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},

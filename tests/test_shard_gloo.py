@@ -54,14 +54,14 @@ def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
     return x, taps, pre, k0, y_full
 
 
-def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1):
+def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, serial=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from vector_amd.shard import ChainConfig, StreamChain
         x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L)
         cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre,
-                          pipeline=pipeline)
+                          pipeline=pipeline, serial=serial)
         be = OracleBackend(cfg)
 
         class PlantingBackend(OracleBackend):
@@ -96,14 +96,15 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,pipeline", [(2, 1), (3, 1), (2, 4), (1, 4)])
-def test_sharded_chain_matches_single_stream(world, pipeline):
+@pytest.mark.parametrize("world,pipeline,serial", [(2, 1, False), (3, 1, False), (2, 4, False),
+                                                   (1, 4, False), (2, 4, True), (3, 2, True)])
+def test_sharded_chain_matches_single_stream(world, pipeline, serial):
     n_local, decim, nfft, ntaps, L = 4096, 2, 256, 31, 100
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline))
+                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline, serial))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -5,12 +5,13 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import vector_amd as va
 from vector_amd import dsp
 ctx = va.get_context(0)
+ctx.bind_stream()
 iters = 20
 for key in (-1024, -2048, 4096, 8192, 16384, -16384):
     N = abs(key)
     frames = max(1, (1 << 28) // N // 8)      # 2**25 points per launch
     io = torch.randn(frames * N, dtype=torch.complex64, device="cuda")
-    for twl in (0, 1):
+    for twl in ((0, 1, 2, 3) if key == 8192 else (0, 1)):
         ctx.check(ctx.lib.vsig_fft_bench(ctx.h, key, dsp._ptr(io), frames, 1, twl), "warm")
         torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -37,4 +37,9 @@ for v, name in ((0, "probe_8B"), (1, "probe_8B_nt"), (2, "probe_16B"), (3, "prob
     for grid in (0, 2048, 16384):
         ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, grid), "c"))
         res[f"{name}_g{grid}"] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
+for v in range(4, 16):
+    U = (2, 4, 8)[(v - 4) // 4]
+    name = f"probe_u{U}_16B" + ("_ntl" if v & 2 else "") + ("_nts" if v & 1 else "")
+    ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
+    res[name] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
 print(json.dumps(res))

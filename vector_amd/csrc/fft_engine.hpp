@@ -516,6 +516,44 @@ __device__ __forceinline__ void fft_frame_anch(float2* v, float2* lds, float2* w
   fft_tail<P, 1>(v, lds, TwAnchors{wa}, t);
 }
 
+// Two independent frames a, d through one LDS buffer, interleaved so that every
+// LDS store of one frame is followed by register work of the other (the store
+// drains while the butterflies issue; the barrier's lgkmcnt(0) then finds it
+// done; left to the scheduler: pinning that order with sched_barrier / register
+// fences measured slower).  Same barrier count as two back-to-back fft_frame calls:
+//   stage0(a) store(a) stage0(d) | B load(a) B store(d) stage1(a) | B load(d) B
+//   store(a) stage1(d) | ... | B load(d) stageL(d)
+// Begins with a barrier (the buffer's previous readers are done).
+template <class P, int p, class TW>
+__device__ __forceinline__ void fft_pair_tail(float2* a, float2* d, float2* lds, TW tws, int t) {
+  // entry: LDS holds a's pass p-1 output; d finished stage p-1 in registers
+  __syncthreads();
+  fft_load<P, p>(a, lds, t);
+  __syncthreads();
+  fft_store<P, p - 1>(d, lds, t);
+  fft_stage<P, p>(a, tws, t);
+  __syncthreads();
+  fft_load<P, p>(d, lds, t);
+  if constexpr (p + 1 < P::NP) {
+    __syncthreads();
+    fft_store<P, p>(a, lds, t);
+    fft_stage<P, p>(d, tws, t);
+    fft_pair_tail<P, p + 1>(a, d, lds, tws, t);
+  } else {
+    fft_stage<P, p>(d, tws, t);
+  }
+}
+
+template <class P, class TW>
+__device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW tws, int t) {
+  static_assert(P::valid() && P::NP >= 2, "invalid FFT plan");
+  __syncthreads();
+  fft_stage<P, 0>(a, tws, t);
+  fft_store<P, 0>(a, lds, t);
+  fft_stage<P, 0>(d, tws, t);
+  fft_pair_tail<P, 1>(a, d, lds, tws, t);
+}
+
 // Index helpers for the operand / result layout.
 template <class P>
 __device__ __forceinline__ int in_index(int t, int e) {          // pass-0 operand e of thread t

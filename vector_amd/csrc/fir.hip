@@ -17,7 +17,7 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e) - lo;
-      if (i >= 0 && i < lim) yb[(unsigned)i] = cconj(v[e]);
+      if (i >= 0 && i < lim) st_stream(yb + (unsigned)i, cconj(v[e]));
     }
   } else {
     // i / decim by a multiply-high with m = floor(2^32 / decim) + 1: exact for
@@ -28,7 +28,7 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e) - lo;
       const unsigned q = __umulhi((unsigned)i, mg);
-      if (i >= 0 && i < lim && (unsigned)i == q * (unsigned)decim) yb[q] = cconj(v[e]);
+      if (i >= 0 && i < lim && (unsigned)i == q * (unsigned)decim) st_stream(yb + q, cconj(v[e]));
     }
   }
 }

@@ -7,6 +7,37 @@
 #include "vsig_kernels.h"
 
 namespace vsig {
+
+// Streaming accesses (input read once, output written once): non-temporal
+// hints keep them from displacing reused lines (filter / template spectra,
+// neighbouring segments' overlap) in L2 / the Infinity Cache.
+#ifndef VSIG_NT_LD
+#define VSIG_NT_LD 0
+#endif
+#ifndef VSIG_NT_ST
+#define VSIG_NT_ST 0
+#endif
+__device__ __forceinline__ float2 ld_stream(const float2* p) {
+#if VSIG_NT_LD
+  return fromv(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
+#else
+  return *p;
+#endif
+}
+__device__ __forceinline__ void st_stream(float2* p, float2 v) {
+#if VSIG_NT_ST
+  __builtin_nontemporal_store(tov(v), reinterpret_cast<f2v*>(p));
+#else
+  *p = v;
+#endif
+}
+__device__ __forceinline__ void st_stream(float* p, float v) {
+#if VSIG_NT_ST
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
 // Occupancy request (min waves per SIMD) of a kernel variant: the split
 // exchange (variant 4) exists to fit two 16k / four 8k frames per CU, which
 // needs <= 128 VGPRs, so ask the register allocator for 4 waves/SIMD there.
@@ -41,13 +72,13 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
   const float2* base = x + s0;
   if (s0 >= 0 && s0 + P::N <= n) {
 #pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = base[(unsigned)in_index<P>(t, e)];
+    for (int e = 0; e < P::E; ++e) v[e] = ld_stream(base + (unsigned)in_index<P>(t, e));
   } else {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = in_index<P>(t, e);
       const long long xi = s0 + i;
-      v[e] = (xi >= 0 && xi < n) ? base[i] : make_float2(0.f, 0.f);
+      v[e] = (xi >= 0 && xi < n) ? ld_stream(base + i) : make_float2(0.f, 0.f);
     }
   }
 }

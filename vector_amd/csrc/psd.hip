@@ -26,7 +26,7 @@ __device__ __forceinline__ void psd_load(float2* v, const float2* __restrict__ x
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = in_index<P>(t, e);
-    v[e] = (active && i < nperseg) ? xf[(long long)i * stride] : make_float2(0.f, 0.f);
+    v[e] = (active && i < nperseg) ? ld_stream(xf + (long long)i * stride) : make_float2(0.f, 0.f);
   }
 }
 
@@ -64,7 +64,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
       }
     }
     return;
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
       }
     }
     return;
@@ -111,7 +111,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
       }
     }
     return;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
         for (int e = 0; e < P::E; ++e) {
           const int i = out_index<P>(t, e);
           const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-          of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+          st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
         }
       }
 #pragma unroll
@@ -169,7 +169,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        of[o] = (v[e].x * v[e].x + v[e].y * v[e].y) * scale;
+        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
       }
     }
 #pragma unroll
@@ -232,8 +232,55 @@ __global__ __launch_bounds__(os_threads<P>()) void fft_bench_kernel(float2* __re
   for (int e = 0; e < P::E; ++e) f[out_index<P>(t, e)] = v[e];
 }
 
+// The correlator's engine configuration: register twiddle anchors, two blocks
+// per CU; PAIR = 1: two frames per block through fft_pair (the half-frame
+// correlator's inner loop without its loads, multiply and epilogue).
+template <class P, int PAIR>
+__global__ __launch_bounds__(P::TF, 2) void fft_bench_anch_kernel(float2* __restrict__ io, int iters,
+                                                                  const float2* __restrict__ tw) {
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 a[P::E], d[P::E];
+  float2* f = io + (long long)blockIdx.x * P::N * (PAIR ? 2 : 1);
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    a[e] = f[in_index<P>(t, e)];
+    d[e] = PAIR ? f[P::N + in_index<P>(t, e)] : make_float2(0.f, 0.f);
+  }
+  for (int it = 0; it < iters; ++it) {
+    if constexpr (PAIR) {
+      launder_anchors<P>(wa);
+      fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+    } else {
+      fft_frame_anch<P>(a, lds, wa, t);
+    }
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      a[e] = make_float2(a[e].x * 1e-4f, a[e].y * 1e-4f);
+      if (PAIR) d[e] = make_float2(d[e].x * 1e-4f, d[e].y * 1e-4f);
+    }
+  }
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    f[out_index<P>(t, e)] = a[e];
+    if (PAIR) f[P::N + out_index<P>(t, e)] = d[e];
+  }
+}
+
 hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const float2* tw, int twl,
                             hipStream_t st) {
+  if (twl >= 2) {          // anchors (2) / anchors + pair (3), 8192-point plan only
+    if (key != 8192) return hipErrorInvalidValue;
+    if (twl == 3)
+      hipLaunchKernelGGL((fft_bench_anch_kernel<Plan8192, 1>), dim3(frames / 2), dim3(Plan8192::TF), 0,
+                         st, io, iters, tw);
+    else
+      hipLaunchKernelGGL((fft_bench_anch_kernel<Plan8192, 0>), dim3(frames), dim3(Plan8192::TF), 0,
+                         st, io, iters, tw);
+    return hipGetLastError();
+  }
 #define VSIG_FB(PL)                                                                          \
   {                                                                                          \
     auto k = twl ? fft_bench_kernel<PL, 1> : fft_bench_kernel<PL, 0>;                         \

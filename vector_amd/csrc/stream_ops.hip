@@ -174,8 +174,49 @@ __global__ __launch_bounds__(256) void copy_probe(const float2* __restrict__ x, 
   }
 }
 
+// Unrolled form: each thread moves U consecutive float4 per iteration with all
+// U loads issued before the first store (U * 16 B in flight per lane), loads
+// and/or stores non-temporal; block-contiguous chunks (no grid stride).
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void copy_probe_u(const f4v* __restrict__ x, long long n4,
+                                                    f4v* __restrict__ y) {
+  const long long base = ((long long)blockIdx.x * 256) * U + threadIdx.x;
+  f4v v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * 256;
+    if (i < n4) v[u] = NTL ? __builtin_nontemporal_load(x + i) : x[i];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * 256;
+    if (i < n4) {
+      if constexpr (NTS) __builtin_nontemporal_store(v[u], y + i);
+      else y[i] = v[u];
+    }
+  }
+}
+
 hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
                              hipStream_t st) {
+  if (variant >= 4) {       // unrolled probes: 4 + (U index)*4 + NTL*2 + NTS
+    const long long n4 = n / 2;
+    const int ui = (variant - 4) / 4, ntl = (variant >> 1) & 1, nts = variant & 1;
+    const int U = ui == 0 ? 2 : ui == 1 ? 4 : 8;
+    const dim3 g((unsigned)((n4 + 256LL * U - 1) / (256LL * U))), b(256);
+    const f4v* x4 = reinterpret_cast<const f4v*>(x);
+    f4v* y4 = reinterpret_cast<f4v*>(y);
+#define VSIG_CPU_(UU)                                                                   \
+    if (ntl && nts) hipLaunchKernelGGL((copy_probe_u<UU, true, true>), g, b, 0, st, x4, n4, y4);  \
+    else if (ntl) hipLaunchKernelGGL((copy_probe_u<UU, true, false>), g, b, 0, st, x4, n4, y4);   \
+    else if (nts) hipLaunchKernelGGL((copy_probe_u<UU, false, true>), g, b, 0, st, x4, n4, y4);   \
+    else hipLaunchKernelGGL((copy_probe_u<UU, false, false>), g, b, 0, st, x4, n4, y4);
+    if (U == 2) { VSIG_CPU_(2) } else if (U == 4) { VSIG_CPU_(4) } else { VSIG_CPU_(8) }
+#undef VSIG_CPU_
+    (void)grid;
+    return hipGetLastError();
+  }
   const dim3 g(grid > 0 ? grid : 8192), b(256);
   switch (variant) {
     case 0: hipLaunchKernelGGL((copy_probe<8, false>), g, b, 0, st, x, n, y); break;

@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{16, 8, 65};         // tuned defaults (see vsig_set_option)
+  vsig::Variants var{16, 8, 193};        // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
   int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
@@ -351,7 +351,7 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   const std::string k(key);
   if (k == "psd_variant") c->var.psd = value & 29;
   else if (k == "fir_variant") c->var.fir = value & 31;
-  else if (k == "xcorr_variant") c->var.xcorr = value & 127;
+  else if (k == "xcorr_variant") c->var.xcorr = value & 255;
   else if (k == "fir_m" || k == "xcorr_m") {
     if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
         value != 16384)
@@ -385,7 +385,7 @@ int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
 int vsig_fft_bench(vsig_ctx* c, int key, void* io, int frames, int iters, int twl) {
   if (!c || !io || frames < 1 || iters < 1) return fail(c, VSIG_E_INVALID, "bad arguments");
   const float2* tw;
-  int rc = twl ? get_tw2(c, key, &tw) : get_twiddles(c, key, &tw);
+  int rc = twl == 1 ? get_tw2(c, key, &tw) : get_twiddles(c, key, &tw);
   if (rc) return rc;
   Timed t(c, "fft_bench");
   HIPCHK(c, vsig::launch_fft_bench(key, (float2*)io, frames, iters, tw, twl, c->stream));

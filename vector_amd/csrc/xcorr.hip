@@ -246,8 +246,21 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     s1 += ok ? __builtin_amdgcn_sqrtf(a2r) : 0.f;
     s2 += ok ? a2r : 0.f;
   };
+  if (!rev && lim > H) {
+    // every index of the a half is valid (< H < lim): no masks, strict '>'
 #pragma unroll
-  for (int e = 0; e < P::E; ++e) acc(a[e], out_index<P>(t, e));
+    for (int e = 0; e < P::E; ++e) {
+      const float a2 = a[e].x * a[e].x + a[e].y * a[e].y;
+      const bool take = a2 > m;
+      m = take ? a2 : m;
+      mi = take ? out_index<P>(t, e) : mi;
+      s1 += __builtin_amdgcn_sqrtf(a2);
+      s2 += a2;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) acc(a[e], out_index<P>(t, e));
+  }
 #pragma unroll
   for (int e = 0; e < P::E; ++e) acc(d[e], out_index<P>(t, e) + H);
   wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
@@ -255,8 +268,10 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
 
 // TW: twiddle source of the passes: 0 the global per-pass table, 1 the
 // two-level LDS table, 2 per-thread register anchors (no loads inside the
-// transforms; see TwAnchors in fft_engine.hpp).
-template <class P, int TW>
+// transforms; see TwAnchors in fft_engine.hpp).  PAIR: the two halves go
+// through fft_pair (LDS stores of one half overlap the other's butterflies)
+// instead of two back-to-back fft_frame calls.
+template <class P, int TW, int PAIR>
 __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
@@ -279,8 +294,23 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
     else if constexpr (TW == 2) fft_frame_anch<P>(v, lds, wa, t);
     else fft_frame<P>(v, lds, tw, t);
   };
+  auto fft2 = [&](float2* x, float2* y) {
+    if constexpr (PAIR) {
+      if constexpr (TW == 1) fft_pair<P>(x, y, lds, TwLds{t2 + opaque_zero()}, t);
+      else if constexpr (TW == 2) { launder_anchors<P>(wa); fft_pair<P>(x, y, lds, TwAnchors{wa}, t); }
+      else fft_pair<P>(x, y, lds, TwTable{tw + opaque_zero()}, t);
+    } else {
+      fft(x);
+      fft(y);
+    }
+  };
   float2 a[P::E], d[P::E];
+#ifdef VSIG_EXP_NO_LOAD      // timing experiments only (results are wrong)
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) { a[e] = make_float2((float)(t + e), (float)(b & 7)); d[e] = make_float2((float)e, 1.f); }
+#else
   load_halves<P>(a, d, s, b * hop - off, n, t);
+#endif
   const float2 w = wt[t];
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
@@ -288,16 +318,18 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
     a[e] = cadd(x0, x1);
     d[e] = twc<half_root<P, M>(e), 64>(cmul(csub(x0, x1), w));
   });
-  fft(a);
-  fft(d);
+  fft2(a, d);
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
+#ifdef VSIG_EXP_NO_PS
+    const float4 p = make_float4(0.5f, 0.25f, 0.125f, 0.5f);
+#else
     const float4 p = Ps2[out_index<P>(t, e)];
+#endif
     a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
     d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
   }
-  fft(a);
-  fft(d);
+  fft2(a, d);
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 o = twc<half_root<P, M>(e), 64>(cmul(d[e], w));
@@ -305,7 +337,14 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
   });
+#ifdef VSIG_EXP_NO_EPI
+  float acc = 0.f;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) acc += a[e].x + a[e].y + d[e].x + d[e].y;
+  if (acc == 12345.f) partials[b].sum_abs = acc;
+#else
   xcorr_half_epilogue<P>(a, d, b, hop, nout, c, store_mode, partials, t);
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -318,7 +357,7 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
 // of the 4L-point FFTs plain overlap-save needs for the same efficiency.
 // ---------------------------------------------------------------------------
 template <class P, int TWL>
-__global__ __launch_bounds__(os_threads<P>(), 3) void xcorr_part_kernel(
+__global__ __launch_bounds__(os_threads<P>(), 2) void xcorr_part_kernel(
     const float2* __restrict__ s, long long n, const float2* __restrict__ P0,
     const float2* __restrict__ P1, long long off, long long nout, int Lp, long long nhops,
     long long hpb, float2* __restrict__ c, int store_mode, PeakPartial* __restrict__ partials,
@@ -378,9 +417,13 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
   if ((variant & 64) && M == 16384) {   // half-frame kernel, two blocks per CU
-    auto k = (variant & 8)   ? xcorr_half_kernel<Plan8192, 1>
-             : (variant & 1) ? xcorr_half_kernel<Plan8192, 2>
-                             : xcorr_half_kernel<Plan8192, 0>;
+    auto k = (variant & 128)
+                 ? ((variant & 8)   ? xcorr_half_kernel<Plan8192, 1, 1>
+                    : (variant & 1) ? xcorr_half_kernel<Plan8192, 2, 1>
+                                    : xcorr_half_kernel<Plan8192, 0, 1>)
+                 : ((variant & 8)   ? xcorr_half_kernel<Plan8192, 1, 0>
+                    : (variant & 1) ? xcorr_half_kernel<Plan8192, 2, 0>
+                                    : xcorr_half_kernel<Plan8192, 0, 0>);
     hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(Plan8192::TF), 0, st, s, n,
                        reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
                        partials, nblocks, tw, wt);

@@ -45,6 +45,8 @@ class ChainConfig:
     template: np.ndarray | None = None   # sync preamble (None: no xcorr stage)
     window: str = "hann"
     pipeline: int = 1            # sub-chunks per step (FIR / PSD / xcorr overlap on 3 streams)
+    serial: bool = False         # sub-chunks in order on one stream: FIR(k+1), PSD(k), xcorr(k)
+                                 # (a sub-chunk's filtered samples are re-read while cache-resident)
 
     def validate(self, world: int):
         ny = self.n_local // self.decim
@@ -191,6 +193,8 @@ class StreamChain:
                 req.wait()
 
     def step(self):
+        if self.cfg.serial:
+            return self._step_serial()
         r, w, K = self.rank, self.world, self.cfg.pipeline
         be = self.be
         n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
@@ -230,6 +234,50 @@ class StreamChain:
             be.join()
         if L:
             if w > 1:                           # 6. global peak records
+                rows = [torch.empty_like(self.recs) for _ in range(w)]
+                dist.all_gather(rows, self.recs, group=self.group)
+                self.peak_rows = rows
+            else:
+                self.peak_rows = [self.recs]
+
+    def _step_serial(self):
+        """The same step with the sub-chunks run in order on the current stream,
+        PSD(k) and xcorr(k) right after FIR(k+1) (xcorr(k) needs the first L-1
+        filtered samples of sub-chunk k+1): each sub-chunk's filtered stream is
+        re-read soon after it is written instead of a whole chunk later."""
+        r, w, K = self.rank, self.world, self.cfg.pipeline
+        be = self.be
+        n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
+        nk, nyk = n // K, ny // K
+        if w > 1 and hist > 0:                  # left halo of the input
+            self._exchange(self.x_ext[n: n + hist] if r < w - 1 else None,
+                           r + 1 if r < w - 1 else None,
+                           self.x_ext[: hist] if r > 0 else None,
+                           r - 1 if r > 0 else None)
+
+        def fir(k):
+            be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
+                        self.y_ext[k * nyk: (k + 1) * nyk])
+
+        def consume(k):
+            be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
+            if L:
+                last = k == K - 1
+                halo = (L - 1) if (not last or r < w - 1) else 0
+                be.xcorr_peak(self.y_ext[k * nyk: (k + 1) * nyk + halo], self.recs[k])
+
+        fir(0)
+        if w > 1 and L > 1:                     # right halo of the filtered stream
+            self._exchange(self.y_ext[: L - 1] if r > 0 else None,
+                           r - 1 if r > 0 else None,
+                           self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
+                           r + 1 if r < w - 1 else None)
+        for k in range(1, K):
+            fir(k)
+            consume(k - 1)
+        consume(K - 1)
+        if L:
+            if w > 1:
                 rows = [torch.empty_like(self.recs) for _ in range(w)]
                 dist.all_gather(rows, self.recs, group=self.group)
                 self.peak_rows = rows
