@@ -56,6 +56,39 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fi
 
   const int lo = ntaps - 1;
   const long long nloc = n - g0;
+  if constexpr (PERSIST == 5) {      // one unit per block, register twiddle anchors
+    float2 wa[nanch_total<P>()];
+    load_anchors<P>(wa, tw, t);
+    float2 v[P::E];
+    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
+    fft_frame_anch<P>(v, lds, wa, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
+    fft_frame_anch<P>(v, lds, wa, t);
+    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
+    return;
+  }
+  if constexpr (PERSIST == 6) {      // two consecutive units per block (fft_pair), anchors
+    float2 wa[nanch_total<P>()];
+    load_anchors<P>(wa, tw, t);
+    const long long b0 = 2 * b, b1 = 2 * b + 1;
+    float2 a[P::E], d[P::E];
+    load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
+    load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
+    launder_anchors<P>(wa);
+    fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const float2 h = Hs[out_index<P>(t, e)];
+      a[e] = cconj(cmul(a[e], h));
+      d[e] = cconj(cmul(d[e], h));
+    }
+    launder_anchors<P>(wa);
+    fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+    fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
+    fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
+    return;
+  }
   if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
     float2* t2 = lds + (P::LDS + 1) / 2;
     float* ldf = reinterpret_cast<float*>(lds);
@@ -134,7 +167,8 @@ void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, 
                   hipStream_t st) {
   const long long grid =
       (PERSIST == 1 || PERSIST == 2)
-          ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks) : nblocks;
+          ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks)
+          : PERSIST == 6 ? (nblocks + 1) / 2 : nblocks;
   hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(os_threads<PL>()),
                      0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
 }
@@ -145,8 +179,11 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
   VSIG_OS_SWITCH(M, variant, {
+    // (bits 3/4 first: they select the two-level twiddle table the API built)
     if (variant & 16) launch_fir_t<PL, 4>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 64) launch_fir_t<PL, 6>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 32) launch_fir_t<PL, 5>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 4) launch_fir_t<PL, 2>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else launch_fir_t<PL, 0>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);

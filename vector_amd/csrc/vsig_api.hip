@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{16, 8, 193};        // tuned defaults (see vsig_set_option)
+  vsig::Variants var{16, 64, 193};       // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
   int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
@@ -95,7 +95,6 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
 // Twiddle-table key of the plan an overlap-save launch of size M uses.
 int tw_key(int M, int variant) {
   if (M == 1024 || M == 2048) return -M;           // one-wave plans
-  if (M == 16384 && (variant & 64)) return 8192;   // half-frame correlator: 8192-point plan
   return (M == 16384 && (variant & 2)) ? -16384 : M;
 }
 
@@ -261,13 +260,15 @@ int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, co
   int rc = ensure_partials(c, nparts);
   if (rc) return rc;
   const float2* tw;
-  rc = get_tw_for(c, M, var, true, &tw);
-  if (rc) return rc;
   const float2* wt = nullptr;
-  if (!Ps1 && M == 16384 && (var & 64)) {
-    rc = get_half_tw(c, M, 256, &wt);
+  if (!Ps1 && M == 16384 && (var & 64)) {    // half-frame correlator: 8192-point plan
+    rc = (var & 8) ? get_tw2(c, 8192, &tw) : get_twiddles(c, 8192, &tw);
     if (rc) return rc;
+    rc = get_half_tw(c, M, 256, &wt);
+  } else {
+    rc = get_tw_for(c, M, var, true, &tw);
   }
+  if (rc) return rc;
   {
     Timed t(c, "xcorr");
     if (Ps1)
@@ -350,7 +351,7 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   if (!c || !key) return VSIG_E_INVALID;
   const std::string k(key);
   if (k == "psd_variant") c->var.psd = value & 29;
-  else if (k == "fir_variant") c->var.fir = value & 31;
+  else if (k == "fir_variant") c->var.fir = value & 127;
   else if (k == "xcorr_variant") c->var.xcorr = value & 255;
   else if (k == "fir_m" || k == "xcorr_m") {
     if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
