@@ -288,7 +288,7 @@ def test_correlator_stream_full_size_property(gpu):
     assert peak == pytest.approx(direct, rel=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40, 64, 65, 72, 96, 192, 193])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40, 64, 65, 72, 96, 192, 193, 224])
 def test_kernel_variants_agree_with_oracle(gpu, variant):
     """Every tuning variant (persistent / LDS twiddles / split exchange /
     512-thread 16k plan) must give the same results as the oracle."""

@@ -44,6 +44,40 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
   const long long units = (nframes + FPB - 1) / FPB;
   long long u = blockIdx.x;
   if (u >= units) return;
+  if constexpr (PERSIST == 5 || PERSIST == 6) {   // register twiddle anchors; 6: two frames (fft_pair)
+    if constexpr (FPB != 1) return;                // launch_psd only picks these for TF >= 256
+    constexpr int NF = PERSIST == 6 ? 2 : 1;
+    float2 wa[nanch_total<P>()];
+    load_anchors<P>(wa, tw, t);
+    float2 v[NF][P::E];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      psd_load<P>(v[f], x, stride, nperseg, hop, u * NF + f, nframes, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = in_index<P>(t, e);
+        const float w = i < nperseg ? win[i] : 0.f;
+        v[f][e] = make_float2(v[f][e].x * w, v[f][e].y * w);
+      }
+    }
+    launder_anchors<P>(wa);
+    if constexpr (NF == 2) fft_pair<P>(v[0], v[1], lds, TwAnchors{wa}, t);
+    else fft_frame_anch<P>(v[0], lds, wa, t);
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      const long long frame = u * NF + f;
+      if (frame < nframes) {
+        float* of = out + frame * P::N;
+#pragma unroll
+        for (int e = 0; e < P::E; ++e) {
+          const int i = out_index<P>(t, e);
+          const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+          __builtin_nontemporal_store((v[f][e].x * v[f][e].x + v[f][e].y * v[f][e].y) * scale, of + o);
+        }
+      }
+    }
+    return;
+  }
   if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
     constexpr int FL = (P::LDS + 1) / 2;
     float2* t2 = lds + FPB * FL;
@@ -64,7 +98,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
+        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
       }
     }
     return;
@@ -88,7 +122,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
+        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
       }
     }
     return;
@@ -111,7 +145,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
+        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
       }
     }
     return;
@@ -137,7 +171,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
         for (int e = 0; e < P::E; ++e) {
           const int i = out_index<P>(t, e);
           const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-          st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
+          __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
         }
       }
 #pragma unroll
@@ -169,7 +203,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
       for (int e = 0; e < P::E; ++e) {
         const int i = out_index<P>(t, e);
         const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        st_stream(of + o, (v[e].x * v[e].x + v[e].y * v[e].y) * scale);
+        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
       }
     }
 #pragma unroll
@@ -307,7 +341,8 @@ void launch_psd_t(const float2* x, long long stride, const float* win, int npers
   constexpr int FPB = BT / PL::TF;
   const long long units = (nframes + FPB - 1) / FPB;
   const long long grid =
-      (PERSIST == 1 || PERSIST == 2) ? persistent_grid(psd_kernel<PL, PERSIST>, BT, units) : units;
+      (PERSIST == 1 || PERSIST == 2) ? persistent_grid(psd_kernel<PL, PERSIST>, BT, units)
+      : PERSIST == 6 ? (units + 1) / 2 : units;
   hipLaunchKernelGGL((psd_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(BT), 0, st, x, stride,
                      win, nperseg, hop, scale, out, nframes, shift, tw);
 }
@@ -317,7 +352,12 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                       const float2* tw, int variant, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
   VSIG_PLAN_SWITCH(N, {
-    if (variant & 16) launch_psd_t<PL, 4>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    // bits 5/6 (anchors, frame pairs) need one frame per block (TF >= 256);
+    // smaller plans take the split-exchange kernel instead.
+    const bool big = PL::TF >= 256;
+    if ((variant & 64) && big) launch_psd_t<PL, 6>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    else if ((variant & 32) && big) launch_psd_t<PL, 5>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    else if (variant & (16 | 32 | 64)) launch_psd_t<PL, 4>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else if (variant & 8) launch_psd_t<PL, 3>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else if (variant & 4) launch_psd_t<PL, 2>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
     else if (variant & 1) launch_psd_t<PL, 1>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);

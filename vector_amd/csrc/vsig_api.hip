@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{16, 64, 193};       // tuned defaults (see vsig_set_option)
+  vsig::Variants var{64, 64, 193};       // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
   int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
@@ -350,7 +350,7 @@ int vsig_set_stream(vsig_ctx* c, void* s) {
 int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   if (!c || !key) return VSIG_E_INVALID;
   const std::string k(key);
-  if (k == "psd_variant") c->var.psd = value & 29;
+  if (k == "psd_variant") c->var.psd = value & 125;
   else if (k == "fir_variant") c->var.fir = value & 127;
   else if (k == "xcorr_variant") c->var.xcorr = value & 255;
   else if (k == "fir_m" || k == "xcorr_m") {
@@ -440,7 +440,12 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
     return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
   const float2* tw;
-  int rc = get_tw_for(c, nfft, c->var.psd, false, &tw);
+  // anchor / pair variants (bits 5, 6) read the per-pass table and run for
+  // plans of >= 256 threads (nfft >= 8192); below that they fall back to the
+  // split-exchange kernel and its two-level table (see launch_psd)
+  const int pv = c->var.psd;
+  const bool anch = (pv & 96) && nfft >= 8192;
+  int rc = (!anch && (pv & (8 | 16 | 32 | 64))) ? get_tw2(c, nfft, &tw) : get_twiddles(c, nfft, &tw);
   if (rc) return rc;
   Timed t(c, "psd");
   HIPCHK(c, vsig::launch_psd(nfft, (const float2*)x, stride, win, nperseg, hop, scale, sxx, nframes,
