@@ -311,7 +311,7 @@ def test_kernel_variants_agree_with_oracle(gpu, variant):
             gpu.dsp._fir_cache.clear()
             assert_normwise(gpu.filter(x, taps, 1), ref.fir_filter(x, taps, 1), FIR_TOL)
             assert_normwise(gpu.filter(x, taps, 3), ref.fir_filter(x, taps, 3), FIR_TOL)
-        for nfft in (1024, 8192, 16384):
+        for nfft in (1024, 4096, 8192, 16384):
             _, _, S = gpu.spectrum(x, 1.0, "hann", nfft, nfft // 4, nfft)
             _, _, R = ref.spectrum(x, 1.0, "hann", nfft, nfft // 4, nfft)
             assert_spectra_close(S, R)

@@ -42,4 +42,9 @@ for v in range(4, 16):
     name = f"probe_u{U}_16B" + ("_ntl" if v & 2 else "") + ("_nts" if v & 1 else "")
     ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
     res[name] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
+for v in range(16, 28):
+    U = (4, 8, 16)[(v - 16) // 4]
+    name = f"probe_u{U}_8B" + ("_ntl" if v & 2 else "") + ("_nts" if v & 1 else "")
+    ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
+    res[name] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
 print(json.dumps(res))

@@ -8,39 +8,29 @@
 
 namespace vsig {
 
-// Streaming accesses (input read once, output written once): non-temporal
-// hints keep them from displacing reused lines (filter / template spectra,
-// neighbouring segments' overlap) in L2 / the Infinity Cache.
+// Streaming accesses (input read once, output written once) with a
+// non-temporal hint where it measured faster on the chain: the PSD's frame
+// loads and the FIR's output stores (so the filtered stream does not sit in
+// L2 / the Infinity Cache as dirty lines while the PSD and the correlator
+// read it); the FIR's overlapping segment loads stay plain (NT measured
+// slower there).  VSIG_NT_LD / VSIG_NT_ST force all on (A/B builds).
 #ifndef VSIG_NT_LD
 #define VSIG_NT_LD 0
 #endif
 #ifndef VSIG_NT_ST
 #define VSIG_NT_ST 0
 #endif
+template <bool NT = false>
 __device__ __forceinline__ float2 ld_stream(const float2* p) {
-#if VSIG_NT_LD
-  return fromv(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
-#else
-  return *p;
-#endif
+  if constexpr (NT || VSIG_NT_LD) return fromv(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
+  else return *p;
 }
+template <bool NT = true>
 __device__ __forceinline__ void st_stream(float2* p, float2 v) {
-#if VSIG_NT_ST
-  __builtin_nontemporal_store(tov(v), reinterpret_cast<f2v*>(p));
-#else
-  *p = v;
-#endif
+  if constexpr (NT || VSIG_NT_ST) __builtin_nontemporal_store(tov(v), reinterpret_cast<f2v*>(p));
+  else *p = v;
 }
-__device__ __forceinline__ void st_stream(float* p, float v) {
-#if VSIG_NT_ST
-  __builtin_nontemporal_store(v, p);
-#else
-  *p = v;
-#endif
-}
-// Occupancy request (min waves per SIMD) of a kernel variant: the split
-// exchange (variant 4) exists to fit two 16k / four 8k frames per CU, which
-// needs <= 128 VGPRs, so ask the register allocator for 4 waves/SIMD there.
+
 template <class P, int PERSIST>
 constexpr int min_waves() {
 #ifdef VSIG_EXP_SPLIT_W4

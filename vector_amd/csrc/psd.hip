@@ -26,7 +26,7 @@ __device__ __forceinline__ void psd_load(float2* v, const float2* __restrict__ x
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = in_index<P>(t, e);
-    v[e] = (active && i < nperseg) ? ld_stream(xf + (long long)i * stride) : make_float2(0.f, 0.f);
+    v[e] = (active && i < nperseg) ? ld_stream<true>(xf + (long long)i * stride) : make_float2(0.f, 0.f);
   }
 }
 
@@ -364,6 +364,15 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
     else launch_psd_t<PL, 0>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
   });
   return hipGetLastError();
+}
+
+int psd_plan_threads(int N) {
+  auto f = [](int n, int* tf) -> hipError_t {
+    VSIG_PLAN_SWITCH(n, { *tf = PL::TF; });
+    return hipSuccess;
+  };
+  int tf = 0;
+  return f(N, &tf) == hipSuccess ? tf : 0;
 }
 
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,

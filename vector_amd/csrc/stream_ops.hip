@@ -178,11 +178,12 @@ __global__ __launch_bounds__(256) void copy_probe(const float2* __restrict__ x, 
 // U loads issued before the first store (U * 16 B in flight per lane), loads
 // and/or stores non-temporal; block-contiguous chunks (no grid stride).
 typedef float f4v __attribute__((ext_vector_type(4)));
-template <int U, bool NTL, bool NTS>
-__global__ __launch_bounds__(256) void copy_probe_u(const f4v* __restrict__ x, long long n4,
-                                                    f4v* __restrict__ y) {
+typedef float f2v __attribute__((ext_vector_type(2)));
+template <int U, bool NTL, bool NTS, class V = f4v>
+__global__ __launch_bounds__(256) void copy_probe_u(const V* __restrict__ x, long long n4,
+                                                    V* __restrict__ y) {
   const long long base = ((long long)blockIdx.x * 256) * U + threadIdx.x;
-  f4v v[U];
+  V v[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const long long i = base + (long long)u * 256;
@@ -200,6 +201,21 @@ __global__ __launch_bounds__(256) void copy_probe_u(const f4v* __restrict__ x, l
 
 hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
                              hipStream_t st) {
+  if (variant >= 16) {      // unrolled 8-B probes: 16 + (U index)*4 + NTL*2 + NTS
+    const int ui = (variant - 16) / 4, ntl = (variant >> 1) & 1, nts = variant & 1;
+    const int U = ui == 0 ? 4 : ui == 1 ? 8 : 16;
+    const dim3 g((unsigned)((n + 256LL * U - 1) / (256LL * U))), b(256);
+    const f2v* x2 = reinterpret_cast<const f2v*>(x);
+    f2v* y2 = reinterpret_cast<f2v*>(y);
+#define VSIG_CP8_(UU)                                                                              \
+    if (ntl && nts) hipLaunchKernelGGL((copy_probe_u<UU, true, true, f2v>), g, b, 0, st, x2, n, y2);  \
+    else if (ntl) hipLaunchKernelGGL((copy_probe_u<UU, true, false, f2v>), g, b, 0, st, x2, n, y2);   \
+    else if (nts) hipLaunchKernelGGL((copy_probe_u<UU, false, true, f2v>), g, b, 0, st, x2, n, y2);   \
+    else hipLaunchKernelGGL((copy_probe_u<UU, false, false, f2v>), g, b, 0, st, x2, n, y2);
+    if (U == 4) { VSIG_CP8_(4) } else if (U == 8) { VSIG_CP8_(8) } else { VSIG_CP8_(16) }
+#undef VSIG_CP8_
+    return hipGetLastError();
+  }
   if (variant >= 4) {       // unrolled probes: 4 + (U index)*4 + NTL*2 + NTS
     const long long n4 = n / 2;
     const int ui = (variant - 4) / 4, ntl = (variant >> 1) & 1, nts = variant & 1;

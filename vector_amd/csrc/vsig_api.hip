@@ -441,10 +441,10 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
   const float2* tw;
   // anchor / pair variants (bits 5, 6) read the per-pass table and run for
-  // plans of >= 256 threads (nfft >= 8192); below that they fall back to the
+  // plans of >= 256 threads per frame; below that they fall back to the
   // split-exchange kernel and its two-level table (see launch_psd)
   const int pv = c->var.psd;
-  const bool anch = (pv & 96) && nfft >= 8192;
+  const bool anch = (pv & 96) && vsig::psd_plan_threads(nfft) >= 256;
   int rc = (!anch && (pv & (8 | 16 | 32 | 64))) ? get_tw2(c, nfft, &tw) : get_twiddles(c, nfft, &tw);
   if (rc) return rc;
   Timed t(c, "psd");

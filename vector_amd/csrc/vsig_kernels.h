@@ -48,6 +48,9 @@ struct Variants { int psd, fir, xcorr; };
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
                       long long hop, float scale, float* out, long long nframes, int shift,
                       const float2* tw, int variant, hipStream_t st);
+// Threads per frame of the spectrum plan for N points (0: no plan); the
+// anchor / pair PSD variants need >= 256 (one frame per block).
+int psd_plan_threads(int N);
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
                                 const float2* tw, hipStream_t st);
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
