@@ -43,3 +43,29 @@ def test_stream_chain_matches_oracle(gpu, decim, pipeline, L):
     assert nout == len(yr) - L + 1
     assert m == pytest.approx(peak, rel=1e-4)            # finalized record: max |c|
     assert s1 == pytest.approx(r1, rel=1e-4) and s2 == pytest.approx(r2, rel=1e-4)
+
+
+@pytest.mark.parametrize("decim", [1, 4])
+def test_split_first_fir_matches_single_launch(gpu, decim):
+    """shard.StreamChain._fir_first (a rank > 0 of a multi-GPU run): the bulk of
+    sub-chunk 0 filtered before the left halo lands, the head after it, on the
+    HIP backend -- the same filtered stream as one launch over [halo | chunk]."""
+    import torch
+    from vector_amd.shard import ChainConfig, HipBackend, StreamChain
+    n = 1 << 18
+    taps = scipy.signal.firwin(255, 0.2).astype(np.float32)
+    cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=1024, template=None)
+    be = HipBackend(cfg, 0)
+    ch = StreamChain(cfg, be, 0, 1)
+    x_ext = torch.from_numpy(ref.synth_iq(n + 254, seed=5)).cuda()
+    ch.x_ext.copy_(x_ext)
+    want = torch.empty(n // decim, dtype=torch.complex64, device="cuda")
+    be.fir_into(x_ext, 254, want)
+    # the split as _fir_first issues it (exchange skipped: the halo is already in place)
+    s = -(-254 // decim) * decim
+    be.fir_into(ch.x_ext[s: n + 254], 254, ch.y_ext[s // decim: n // decim])
+    be.fir_into(ch.x_ext[: s + 254], 254, ch.y_ext[: s // decim])
+    torch.cuda.synchronize()
+    got = ch.y.cpu().numpy()
+    w = want.cpu().numpy()
+    assert np.abs(got - w).max() <= 1e-5 * np.abs(w).max()

@@ -544,12 +544,17 @@ __device__ __forceinline__ void fft_pair_tail(float2* a, float2* d, float2* lds,
   }
 }
 
-template <class P, class TW>
-__device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW tws, int t) {
+// hook() runs after a's first stage is stored, before d's first stage: a
+// caller finishing d's operands there (e.g. a spectrum multiply whose loads
+// were issued before the call) overlaps that work's latency with a's stage.
+template <class P, class TW, class H = NoHook>
+__device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW tws, int t,
+                                         H hook = H{}) {
   static_assert(P::valid() && P::NP >= 2, "invalid FFT plan");
   __syncthreads();
   fft_stage<P, 0>(a, tws, t);
   fft_store<P, 0>(a, lds, t);
+  hook();
   fft_stage<P, 0>(d, tws, t);
   fft_pair_tail<P, 1>(a, d, lds, tws, t);
 }

@@ -182,15 +182,41 @@ class StreamChain:
     def y(self):
         return self.y_ext[: self.ny]
 
-    def _exchange(self, send, dst, recv, src):
+    def _exchange_start(self, send, dst, recv, src):
         ops = []
         if send is not None and dst is not None:
             ops.append(dist.P2POp(dist.isend, send, dst, group=self.group))
         if recv is not None and src is not None:
             ops.append(dist.P2POp(dist.irecv, recv, src, group=self.group))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    @staticmethod
+    def _exchange_wait(reqs):
+        for req in reqs:
+            req.wait()
+
+    def _exchange(self, send, dst, recv, src):
+        self._exchange_wait(self._exchange_start(send, dst, recv, src))
+
+    def _fir_first(self, be, nk, nyk):
+        """FIR of sub-chunk 0 with the left-halo exchange hidden behind it:
+        outputs from a decimation-aligned s >= ntaps-1 on need only the rank's
+        own samples and are filtered while the halo is in flight; the first
+        s outputs follow once it has landed."""
+        r, w, hist, n = self.rank, self.world, self.hist, self.cfg.n_local
+        D = self.cfg.decim
+        if not (w > 1 and hist > 0):
+            be.fir_into(self.x_ext[: nk + hist], hist, self.y_ext[: nyk])
+            return
+        reqs = self._exchange_start(self.x_ext[n: n + hist] if r < w - 1 else None,
+                                    r + 1 if r < w - 1 else None,
+                                    self.x_ext[: hist] if r > 0 else None,
+                                    r - 1 if r > 0 else None)
+        s = -(-hist // D) * D
+        if s < nk:
+            be.fir_into(self.x_ext[s: nk + hist], hist, self.y_ext[s // D: nyk])
+        self._exchange_wait(reqs)
+        be.fir_into(self.x_ext[: min(s, nk) + hist], hist, self.y_ext[: min(s, nk) // D])
 
     def step(self):
         if self.cfg.serial:
@@ -203,14 +229,12 @@ class StreamChain:
             be.fork()
         ev_fir, ev_halo = [], None
         with _lane(be, "fir"):
-            if w > 1 and hist > 0:              # 1. left halo of the input
-                self._exchange(self.x_ext[n: n + hist] if r < w - 1 else None,
-                               r + 1 if r < w - 1 else None,
-                               self.x_ext[: hist] if r > 0 else None,
-                               r - 1 if r > 0 else None)
-            for k in range(K):                  # 2. FIR (+ decimation), sub-chunk k
-                be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
-                            self.y_ext[k * nyk: (k + 1) * nyk])
+            for k in range(K):                  # 1-2. left halo + FIR (+ decimation), sub-chunk k
+                if k == 0:
+                    self._fir_first(be, nk, nyk)
+                else:
+                    be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
+                                self.y_ext[k * nyk: (k + 1) * nyk])
                 ev_fir.append(_record(be))
                 if k == 0 and w > 1 and L > 1:  # 3. right halo of the filtered stream
                     self._exchange(self.y_ext[: L - 1] if r > 0 else None,
@@ -249,13 +273,11 @@ class StreamChain:
         be = self.be
         n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
         nk, nyk = n // K, ny // K
-        if w > 1 and hist > 0:                  # left halo of the input
-            self._exchange(self.x_ext[n: n + hist] if r < w - 1 else None,
-                           r + 1 if r < w - 1 else None,
-                           self.x_ext[: hist] if r > 0 else None,
-                           r - 1 if r > 0 else None)
 
         def fir(k):
+            if k == 0:                          # with the left-halo exchange
+                self._fir_first(be, nk, nyk)
+                return
             be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
                         self.y_ext[k * nyk: (k + 1) * nyk])
 
