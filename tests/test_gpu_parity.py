@@ -288,7 +288,7 @@ def test_correlator_stream_full_size_property(gpu):
     assert peak == pytest.approx(direct, rel=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40, 64, 65, 72, 96, 192, 193, 224])
+@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40, 64, 65, 72, 96, 128, 192, 193, 224])
 def test_kernel_variants_agree_with_oracle(gpu, variant):
     """Every tuning variant (persistent / LDS twiddles / split exchange /
     512-thread 16k plan) must give the same results as the oracle."""
@@ -340,3 +340,24 @@ def test_kernel_variants_agree_with_oracle(gpu, variant):
         for k, v in saved.items():
             ctx.lib.vsig_set_option(ctx.h, k.encode(), v)
         gpu.dsp._fir_cache.clear()
+
+
+@pytest.mark.parametrize("decim", [2, 3, 4])
+@pytest.mark.parametrize("n", [1, 777, 100_003, 3 * 16384 + 77])
+def test_decimating_fir_frequency_domain(gpu, decim, n):
+    """fir_variant bit 8: decimation folded into the spectrum (M/D-point
+    inverse transforms) for D = 2 / 4 (D = 3 falls back to the full-rate
+    kernel); same outputs as np.convolve(x, h)[:n][::D], any length."""
+    ctx = gpu.get_context()
+    v = C.c_int()
+    ctx.check(ctx.lib.vsig_get_option(ctx.h, b"fir_variant", C.byref(v)), "get")
+    rng = np.random.default_rng(n + decim)
+    x = ref.synth_iq(n, seed=n)
+    for taps in (rng.standard_normal(255).astype(np.float32), np.hanning(65)[1:-1].astype(np.float32)):
+        try:
+            ctx.check(ctx.lib.vsig_set_option(ctx.h, b"fir_variant", v.value | 256), "set")
+            gpu.dsp._fir_cache.clear()
+            assert_normwise(gpu.filter(x, taps, decim), ref.fir_filter(x, taps, decim), FIR_TOL)
+        finally:
+            ctx.lib.vsig_set_option(ctx.h, b"fir_variant", v.value)
+            gpu.dsp._fir_cache.clear()

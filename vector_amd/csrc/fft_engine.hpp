@@ -248,6 +248,13 @@ struct TwAnchors { const float2* wa; };
 //             block from global memory: LDS latency instead of an L2 round
 //             trip per pass, one extra complex multiply per twiddle.
 struct TwLds { const float2* t2; };
+//  TwRegs   : every twiddle the thread applies, exact (from the table), held in
+//             VGPRs for the life of the block: no loads and no generating
+//             multiplies inside the transforms.  Thread t's butterflies in pass
+//             p are j = t + b*TF, so when TF is a multiple of Ns they share one
+//             k = j mod Ns and one set of R-1 twiddles; small plans (the FIR's
+//             1024 points: 3 + 15 values) fit.
+struct TwRegs { const float2* w; };
 
 constexpr int ilog2c(int n) { int l = 0; while ((1 << l) < n) ++l; return l; }
 template <class P> constexpr int tw2_shift() { return (ilog2c(P::N) + 1) / 2; }
@@ -258,6 +265,32 @@ template <class P> constexpr int tw2_size() { return tw2_hi<P>() + (1 << tw2_shi
 template <class P>
 __device__ __forceinline__ void load_tw2(float2* t2, const float2* __restrict__ g, int tid, int nthreads) {
   for (int i = tid; i < tw2_size<P>(); i += nthreads) t2[i] = g[i];
+}
+
+template <class P>
+constexpr int rtw_nb(int p) { return (P::TF % P::ns(p) == 0) ? 1 : P::E / P::R[p]; }
+template <class P>
+constexpr int rtw_off(int p) {
+  int o = 0;
+  for (int q = 1; q < p; ++q) o += rtw_nb<P>(q) * (P::R[q] - 1);
+  return o;
+}
+template <class P>
+constexpr int rtw_total() { return rtw_off<P>(P::NP) > 0 ? rtw_off<P>(P::NP) : 1; }
+
+// Load thread t's exact twiddles (TwRegs) from the per-pass table.
+template <class P>
+__device__ __forceinline__ void load_rtw(float2* w, const float2* __restrict__ tw, int t) {
+  static_for<1, P::NP>([&](auto pi) {
+    constexpr int p = decltype(pi)::value;
+    constexpr int R = P::R[p], Ns = P::ns(p), NB = rtw_nb<P>(p);
+    static_for<0, NB>([&](auto bi) {
+      constexpr int b = decltype(bi)::value;
+      const int k = (t + b * P::TF) & (Ns - 1);
+#pragma unroll
+      for (int r = 1; r < R; ++r) w[rtw_off<P>(p) + b * (R - 1) + r - 1] = tw[P::twoff(p) + (r - 1) * Ns + k];
+    });
+  });
 }
 
 template <class P>
@@ -305,6 +338,11 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
     const float2* twp = tws.tw + P::twoff(p);
 #pragma unroll
     for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], twp[k + (unsigned)((r - 1) * Ns)]);
+  } else if constexpr (std::is_same<TW, TwRegs>::value) {
+    constexpr int NB = rtw_nb<P>(p);
+    const float2* wp = tws.w + rtw_off<P>(p) + (NB == 1 ? 0 : b) * (R - 1);
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], wp[r - 1]);
   } else if constexpr (std::is_same<TW, TwLds>::value) {
     constexpr int S = tw2_shift<P>();
     constexpr int stride = P::N / (Ns * R);       // W_{Ns R}^{rk} = W_N^{rk stride}
@@ -589,6 +627,10 @@ using Plan16384 = Plan<16384, 16, 16, 4, 16, 16>;
 using Plan16384w = Plan<16384, 32, 32, 16, 32>;
 using Plan1024s = Plan<1024, 16, 16, 4, 16>;
 using Plan2048s = Plan<2048, 32, 8, 32, 8>;
+// Inverse transforms of the decimating FIR (fold of a Plan1024s spectrum by
+// D = 2 / 4, same 64 threads): thread t holds bins t + 64 r of both.
+using Plan512d = Plan<512, 8, 8, 8, 8>;
+using Plan256d = Plan<256, 4, 4, 4, 4, 4>;
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

@@ -68,23 +68,28 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fi
     fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
     return;
   }
-  if constexpr (PERSIST == 6) {      // two consecutive units per block (fft_pair), anchors
-    float2 wa[nanch_total<P>()];
-    load_anchors<P>(wa, tw, t);
+  if constexpr (PERSIST == 6 || PERSIST == 7) {   // two consecutive units per block (fft_pair):
+    // 6: register twiddle anchors; 7: exact per-thread twiddles in registers (TwRegs)
+    constexpr bool RT = PERSIST == 7;
+    float2 wa[RT ? rtw_total<P>() : nanch_total<P>()];
+    if constexpr (RT) load_rtw<P>(wa, tw, t);
+    else load_anchors<P>(wa, tw, t);
     const long long b0 = 2 * b, b1 = 2 * b + 1;
     float2 a[P::E], d[P::E];
     load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
     load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
-    launder_anchors<P>(wa);
-    fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+    auto fft2 = [&]() {
+      if constexpr (RT) fft_pair<P>(a, d, lds, TwRegs{wa}, t);
+      else { launder_anchors<P>(wa); fft_pair<P>(a, d, lds, TwAnchors{wa}, t); }
+    };
+    fft2();
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const float2 h = Hs[out_index<P>(t, e)];
       a[e] = cconj(cmul(a[e], h));
       d[e] = cconj(cmul(d[e], h));
     }
-    launder_anchors<P>(wa);
-    fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+    fft2();
     fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
     fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
     return;
@@ -161,6 +166,84 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fi
   }
 }
 
+// ---------------------------------------------------------------------------
+// Decimating FIR (variant bit 8), decimation in the frequency domain: after
+// FFT_M(segment) x H/M, only every D-th output of the block is wanted, and
+//   y[D n] = sum_{k' < M/D} Yd[k'] W_{M/D}^{-n k'},  Yd[k'] = sum_{m < D} Y[k' + m M/D],
+// so the inverse transform shrinks to M/D points (PD) after an in-register
+// fold (thread t holds Y[t + 64 r] and Yd[t + 64 r'] with r = r' + m E/D).
+// The segment starts lo2 = ceil((ntaps-1)/D)*D samples before the block's
+// first output so kept outputs sit at circular indices D n, n >= lo2/D; hop
+// is a multiple of D.  Two segments per wave (fft_pair), anchors for the
+// M-point transforms, exact register twiddles for the small ones.
+// ---------------------------------------------------------------------------
+template <class P, class PD>
+__global__ __launch_bounds__(P::TF) void fir_dec_kernel(
+    const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs, int lo2,
+    long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
+    const float2* __restrict__ twd) {
+  constexpr int D = P::N / PD::N;
+  static_assert(P::TF == PD::TF && P::E == D * PD::E && P::RL == P::E && PD::R[0] == PD::E,
+                "fold needs thread t to hold bins t + TF r of both plans");
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  const long long b = xcd_remap(blockIdx.x, gridDim.x);
+  if (2 * b >= nblocks) return;
+  const long long nloc = n - g0;
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 wr[rtw_total<PD>()];
+  load_rtw<PD>(wr, twd, t);
+  float2 a[P::E], d[P::E];
+  load_segment<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
+  load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
+  launder_anchors<P>(wa);
+  fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+  float2 ua[PD::E], ud[PD::E];
+#pragma unroll
+  for (int r = 0; r < PD::E; ++r) {
+    float2 sa = make_float2(0.f, 0.f), sd = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int m = 0; m < D; ++m) {
+      const int e = r + m * PD::E;
+      const float2 h = Hs[out_index<P>(t, e)];
+      sa = cadd(sa, cmul(a[e], h));
+      sd = cadd(sd, cmul(d[e], h));
+    }
+    ua[r] = cconj(sa);
+    ud[r] = cconj(sd);
+  }
+  fft_pair<PD>(ua, ud, lds, TwRegs{wr}, t);
+  const int n0 = lo2 / D, n1 = (lo2 + (int)hop) / D;
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const long long bb = 2 * b + f;
+    const long long gb = bb * hop - lo2;          // chunk output of circular index 0
+    float2* yb = y + bb * (hop / D) - n0;
+    const float2* u = f ? ud : ua;
+#pragma unroll
+    for (int e = 0; e < PD::E; ++e) {
+      const int i = out_index<PD>(t, e);
+      if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, cconj(u[e]));
+    }
+  }
+}
+
+hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
+                          int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
+                          hipStream_t st) {
+  if (n - g0 <= 0) return hipSuccess;
+  const long long nblocks = (n - g0 + hop - 1) / hop;
+  const dim3 g((unsigned)((nblocks + 1) / 2)), blk(Plan1024s::TF);
+  if (decim == 4)
+    hipLaunchKernelGGL((fir_dec_kernel<Plan1024s, Plan256d>), g, blk, 0, st, x, n, g0, Hs, lo2, hop, y, nblocks, tw, twd);
+  else if (decim == 2)
+    hipLaunchKernelGGL((fir_dec_kernel<Plan1024s, Plan512d>), g, blk, 0, st, x, n, g0, Hs, lo2, hop, y, nblocks, tw, twd);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 template <class PL, int PERSIST>
 void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, int ntaps,
                   long long hop, int decim, float2* y, long long nblocks, const float2* tw,
@@ -168,7 +251,7 @@ void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, 
   const long long grid =
       (PERSIST == 1 || PERSIST == 2)
           ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks)
-          : PERSIST == 6 ? (nblocks + 1) / 2 : nblocks;
+          : (PERSIST == 6 || PERSIST == 7) ? (nblocks + 1) / 2 : nblocks;
   hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(os_threads<PL>()),
                      0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
 }
@@ -182,6 +265,7 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
     // (bits 3/4 first: they select the two-level twiddle table the API built)
     if (variant & 16) launch_fir_t<PL, 4>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
+    else if (variant & 128) launch_fir_t<PL, 7>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 64) launch_fir_t<PL, 6>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 32) launch_fir_t<PL, 5>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
     else if (variant & 4) launch_fir_t<PL, 2>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);

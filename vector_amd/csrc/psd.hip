@@ -398,6 +398,12 @@ hipError_t plan_info(int N, int* radices, int* npasses) {
     for (int q = 0; q < Plan16384w::NP; ++q) radices[q] = Plan16384w::R[q];
     return hipSuccess;
   }
+  if (N == -512 || N == -256) {     // decimating-FIR inverse plans
+    const int np = N == -512 ? Plan512d::NP : Plan256d::NP;
+    *npasses = np;
+    for (int q = 0; q < np; ++q) radices[q] = N == -512 ? Plan512d::R[q] : Plan256d::R[q];
+    return hipSuccess;
+  }
   if (N == -1024 || N == -2048) {   // one-wave overlap-save plans
     const int np = N == -1024 ? Plan1024s::NP : Plan2048s::NP;
     *npasses = np;

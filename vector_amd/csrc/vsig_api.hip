@@ -30,7 +30,7 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{64, 64, 193};       // tuned defaults (see vsig_set_option)
+  vsig::Variants var{64, 320, 193};       // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
   int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
 };
@@ -351,7 +351,7 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   if (!c || !key) return VSIG_E_INVALID;
   const std::string k(key);
   if (k == "psd_variant") c->var.psd = value & 125;
-  else if (k == "fir_variant") c->var.fir = value & 127;
+  else if (k == "fir_variant") c->var.fir = value & 511;
   else if (k == "xcorr_variant") c->var.xcorr = value & 255;
   else if (k == "fir_m" || k == "xcorr_m") {
     if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
@@ -509,7 +509,21 @@ int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n,
   if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
-  int rc = get_tw_for(c, f->M, c->var.fir, true, &tw);
+  int rc;
+  if ((c->var.fir & 256) && f->M == 1024 && (f->decim == 2 || f->decim == 4)) {
+    // decimation in the frequency domain: M/D-point inverse transforms
+    const float2* twd;
+    if ((rc = get_twiddles(c, -1024, &tw)) || (rc = get_twiddles(c, -1024 / f->decim, &twd))) return rc;
+    const int D = f->decim;
+    const int lo2 = (f->ntaps - 1 + D - 1) / D * D;
+    const long long hop = (long long)(f->M - lo2) / D * D;
+    if (hop < D) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
+    Timed t(c, "fir");
+    HIPCHK(c, vsig::launch_fir_dec(D, (const float2*)x, nhist + n, nhist, f->Hs, lo2, hop, (float2*)y,
+                                   tw, twd, c->stream));
+    return VSIG_OK;
+  }
+  rc = get_tw_for(c, f->M, c->var.fir, true, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,

@@ -53,6 +53,10 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
 int psd_plan_threads(int N);
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
                                 const float2* tw, hipStream_t st);
+// Decimating FIR in the frequency domain (M = 1024, D = 2 / 4; see fir.hip).
+hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
+                          int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
+                          hipStream_t st);
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
                          int variant, hipStream_t st);
