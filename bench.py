@@ -134,8 +134,10 @@ def main():
                     help="sub-chunks per step: FIR / PSD / xcorr overlap on three HIP streams")
     ap.add_argument("--serial", action="store_true",
                     help="run the --pipeline sub-chunks in order on one stream (cache reuse)")
-    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m"):
+    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m", "fir_psd_variant", "psd_grid"):
         ap.add_argument("--" + k.replace("_", "-"), type=int, default=None)
+    ap.add_argument("--fuse", action="store_true",
+                    help="FIR and PSD in one fused launch (D=1, nfft 8192; default: two launches)")
     ap.add_argument("--workload", choices=("chain", "pfb"), default="chain",
                     help="chain: the headline FIR->PSD->xcorr metric; pfb: config 4 channelizer")
     ap.add_argument("--nchan", type=int, default=64)
@@ -164,12 +166,12 @@ def main():
     taps, pre, tmpl = design(args.ntaps, args.template, args.decim)
     from vector_amd._lib import get_context
     ctx0 = get_context(local)
-    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m"):
+    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m", "fir_psd_variant", "psd_grid"):
         v = getattr(args, k)
         if v is not None:
             ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, k.encode(), v), k)
     cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl,
-                      pipeline=args.pipeline, serial=args.serial)
+                      pipeline=args.pipeline, serial=args.serial, fuse=args.fuse)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)
     N = world * n
@@ -207,14 +209,16 @@ def main():
     # per-kernel durations from HIP events on the launch stream
     import ctypes as C
     stages = {}
-    for name in ("fir", "psd", "xcorr"):
+    for name in ("fir", "psd", "fir_psd", "xcorr"):
         tot, cnt = C.c_double(), C.c_int64()
         lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
         if cnt.value:
             stages[name] = tot.value / cnt.value
     ny = n // args.decim
+    # fir_psd (fused): x read + y written + Sxx written; the PSD's re-read of y
+    # is served by L2 / the Infinity Cache (PMC traffic in profiles/ checks it)
     bytes_per_launch = {"fir": 8 * n + 8 * ny, "psd": 8 * ny + 4 * ny,
-                        "xcorr": 8 * (ny + chain.yhalo)}
+                        "fir_psd": 8 * n + 8 * ny + 4 * ny, "xcorr": 8 * (ny + chain.yhalo)}
     m, lag, s1, s2, nout = chain.global_peak()
     check = {"sync_lag": lag, "expected": k0 // args.decim, "ok": bool(lag == k0 // args.decim)}
 
@@ -254,11 +258,18 @@ def main():
         stage_roof["xcorr"].update({"flops": int(flops), "TFLOPs": round(tf, 2),
                                     "valu_peak_TFLOPs": FP32_PEAK_TF,
                                     "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
-    if "fir" in stages and "psd" in stages:
+    # north_star's FIR+FFT target on SURVEY.md §8(d) C2's unfused byte count
+    # (28 B/sample: filter() writes y, spectrum() reads it); with the fused
+    # kernel the HBM bytes actually moved are 20 B/sample (stage "fir_psd")
+    fp_ms = (stages["fir"] + stages["psd"]) if ("fir" in stages and "psd" in stages) \
+        else stages.get("fir_psd")
+    if fp_ms:
         b = bytes_per_launch["fir"] + bytes_per_launch["psd"]
-        t = (stages["fir"] + stages["psd"]) * 1e-3
-        stage_roof["fir+psd"] = {"GBs": round(b / t / 1e9, 1),
-                                 "hbm_frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4)}
+        t = fp_ms * 1e-3
+        stage_roof["fir+psd"] = {"ms": round(fp_ms, 4), "GBs": round(b / t / 1e9, 1),
+                                 "hbm_frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
+                                 "bytes_basis": "28 B/sample (unfused FIR 16 + PSD 12)",
+                                 "fused": "fir_psd" in stages}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_samples, taps, args.nfft, tmpl)
@@ -275,7 +286,7 @@ def main():
                    "samples_per_gpu": n, "total_samples": N, "ntaps": args.ntaps,
                    "decim": args.decim, "nfft": args.nfft, "template": args.template,
                    "parallelism": f"time-chunk x{world} (RCCL halos)",
-                   "pipeline": args.pipeline, "serial": args.serial},
+                   "pipeline": args.pipeline, "serial": args.serial, "fused": chain.fused},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},

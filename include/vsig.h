@@ -84,7 +84,8 @@ int vsig_synchronize(vsig_ctx* ctx);
  *   (next-unit prefetch, register twiddles), bit 1 (M = 16384) 512-thread plan,
  *   bit 3 LDS twiddles, bit 4 split re/im exchange, bit 5 (xcorr) partitioned
  *   template, bit 6 (xcorr, M = 16384) half-frame kernel (two blocks per CU);
- *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule.
+ *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule;
+ *   "fir_psd_variant": bit 0 non-temporal filtered-stream stores in the fused kernel.
  * Plans created afterwards use the new block sizes. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 /* Current value of a tuning knob (same keys as vsig_set_option). */
@@ -121,6 +122,8 @@ int vsig_psd_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* win, int3
  * ntaps in [1, 8192]. */
 int vsig_fir_create(vsig_ctx* ctx, const void* taps, int32_t ntaps, int32_t decim, vsig_fir** out);
 void vsig_fir_free(vsig_fir* fir);
+/* Overlap-save block size M chosen for the taps (0 for a null handle). */
+int vsig_fir_block(const vsig_fir* fir);
 int vsig_fir_exec_dev(vsig_fir* fir, const void* x, int64_t n, void* y, int64_t ny);
 /* Time-chunk form: x points at nhist history samples (the previous chunk's
  * last samples, the left halo) followed by the n samples to filter; y gets the
@@ -130,6 +133,15 @@ int vsig_fir_exec_hist_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t 
                            int64_t ny);
 int vsig_fir_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* taps, int32_t ntaps,
                  int32_t decim, void* y, int64_t ny);
+/* Fused filter -> spectrum of the filtered stream (one launch; the chain's
+ * FIR + PSD stages, utils.py:281-291 applied to np.convolve's output):
+ * y as vsig_fir_exec_hist_dev (decim must be 1), and sxx/nframes as
+ * vsig_psd_c64_dev(y, ny, stride 1, win, nperseg = hop = nfft) with
+ * nframes = ny / nfft.  Supported: nfft = 8192, the 1024-point FIR block
+ * (ntaps <= 342); otherwise VSIG_E_UNSUPPORTED (run the two calls). */
+int vsig_fir_psd_exec_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t n, void* y,
+                          int64_t ny, const float* win, int32_t nfft, float scale, int32_t shift,
+                          float* sxx, int64_t nframes);
 
 /* ---- streaming correlation with a fixed template p of length L (<= 8192):
  * c[o] = sum_{k<L} s[o - off + k] conj(p[k]), mode VALID (off = 0, nout = n-L+1)

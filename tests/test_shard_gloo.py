@@ -54,14 +54,15 @@ def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
     return x, taps, pre, k0, y_full
 
 
-def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, serial=False):
+def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, serial=False,
+            fuse=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from vector_amd.shard import ChainConfig, StreamChain
         x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L)
         cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre,
-                          pipeline=pipeline, serial=serial)
+                          pipeline=pipeline, serial=serial, fuse=fuse)
         be = OracleBackend(cfg)
 
         class PlantingBackend(OracleBackend):
@@ -77,9 +78,18 @@ def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, se
                 if a < b:
                     y[a - lo:b - lo] += torch.from_numpy((6 * pre[a - k0:b - k0]).astype(np.complex64))
 
+            def can_fuse(self, cfg):
+                return fuse
+
+            def fir_psd_into(self, x_ext, nhist, y, sxx):
+                # the fused launch's contract: FIR then the PSD of its output
+                self.fir_into(x_ext, nhist, y)
+                self.psd_into(y, sxx)
+
         ch_holder = []
         be = PlantingBackend(cfg)
         ch = StreamChain(cfg, be, rank, world)
+        assert ch.fused == (fuse and decim == 1 and pipeline == 1 and not serial)
         ch_holder.append(ch)
         ch.x.copy_(torch.from_numpy(x[rank * n_local:(rank + 1) * n_local]))
         ch.step()
@@ -96,15 +106,20 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,pipeline,serial", [(2, 1, False), (3, 1, False), (2, 4, False),
-                                                   (1, 4, False), (2, 4, True), (3, 2, True)])
-def test_sharded_chain_matches_single_stream(world, pipeline, serial):
-    n_local, decim, nfft, ntaps, L = 4096, 2, 256, 31, 100
+@pytest.mark.parametrize("world,pipeline,serial,fuse", [
+    (2, 1, False, False), (3, 1, False, False), (2, 4, False, False), (1, 4, False, False),
+    (2, 4, True, False), (3, 2, True, False), (2, 1, False, True), (3, 1, False, True),
+    (1, 1, False, True)])
+def test_sharded_chain_matches_single_stream(world, pipeline, serial, fuse):
+    """fuse: the fused FIR + PSD launch (decim 1), split at a frame boundary on
+    ranks > 0 so the bulk runs while the left halo is in flight."""
+    n_local, decim, nfft, ntaps, L = 4096, 1 if fuse else 2, 256, 31, 100
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline, serial))
+                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline, serial,
+                               fuse))
              for r in range(world)]
     for p in procs:
         p.start()

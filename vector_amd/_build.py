@@ -15,7 +15,7 @@ ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvsig.so")
 SOURCES = ["psd.hip", "fir.hip", "xcorr.hip", "reduce.hip", "analysis.hip", "pfb.hip",
-           "stream_ops.hip", "vsig_api.hip"]
+           "stream_ops.hip", "firpsd.hip", "vsig_api.hip"]
 HEADERS = ["fft_engine.hpp", "os_common.hpp", "vsig_kernels.h"]
 ARCH = os.environ.get("VSIG_ARCH", "gfx950")
 

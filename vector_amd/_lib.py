@@ -58,6 +58,8 @@ SIGNATURES = {
     "vsig_fir_exec_dev": (C.c_int, [P, P, I64, P, I64]),
     "vsig_fir_exec_hist_dev": (C.c_int, [P, P, I64, I64, P, I64]),
     "vsig_fir_c64": (C.c_int, [P, P, I64, P, I32, I32, P, I64]),
+    "vsig_fir_block": (C.c_int, [P]),
+    "vsig_fir_psd_exec_dev": (C.c_int, [P, P, I64, I64, P, I64, P, I32, F32, I32, P, I64]),
     "vsig_xcorr_create": (C.c_int, [P, P, I32, C.POINTER(P)]),
     "vsig_xcorr_free": (None, [P]),
     "vsig_xcorr_exec_dev": (C.c_int, [P, P, I64, I32, P, P]),

@@ -219,6 +219,31 @@ struct Plan {
 
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
+// A plan whose frame is owned by one wave and whose LDS slice is private to
+// that wave: the engine's exchanges then need only a wave barrier (LDS
+// requests of one wave complete in issue order), so the waves of a
+// multi-wave block run their transforms decoupled (fir_psd_kernel).
+template <class P>
+struct WaveSync : P {
+  static_assert(P::TF <= 64, "wave-private frames only");
+  static constexpr bool WAVE_SYNC = true;
+};
+template <class P, class = void>
+struct wave_sync_of { static constexpr bool value = false; };
+template <class P>
+struct wave_sync_of<P, decltype(void(P::WAVE_SYNC))> { static constexpr bool value = P::WAVE_SYNC; };
+
+template <class P>
+__device__ __forceinline__ void plan_sync() {
+  if constexpr (wave_sync_of<P>::value) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  } else {
+    __syncthreads();
+  }
+}
+
 // 0, but unknown to the optimiser (blocks CSE / LICM across FFT calls).
 __device__ __forceinline__ int opaque_zero() {
   int z = 0;
@@ -470,13 +495,13 @@ __device__ __forceinline__ void fft_load_c(float2* v, const float* lds, int t) {
 template <class P, int p, class TW>
 __device__ __forceinline__ void fft_tail_split(float2* v, float* lds, TW tws, int t) {
   if constexpr (p < P::NP) {
-    __syncthreads();
+    plan_sync<P>();
     fft_store_c<P, p - 1, 0>(v, lds, t);
-    __syncthreads();
+    plan_sync<P>();
     fft_load_c<P, p, 0>(v, lds, t);
-    __syncthreads();
+    plan_sync<P>();
     fft_store_c<P, p - 1, 1>(v, lds, t);
-    __syncthreads();
+    plan_sync<P>();
     fft_load_c<P, p, 1>(v, lds, t);
     fft_stage<P, p>(v, tws, t);
     fft_tail_split<P, p + 1>(v, lds, tws, t);
@@ -494,9 +519,9 @@ __device__ __forceinline__ void fft_frame_split(float2* v, float* lds, const flo
 template <class P, int p, class TW, class H = NoHook>
 __device__ __forceinline__ void fft_tail(float2* v, float2* lds, TW tws, int t, H hook = H{}) {
   if constexpr (p < P::NP) {
-    __syncthreads();               // previous readers of lds are done
+    plan_sync<P>();               // previous readers of lds are done
     fft_store<P, p - 1>(v, lds, t);
-    __syncthreads();
+    plan_sync<P>();
     fft_load<P, p>(v, lds, t);
     fft_stage<P, p>(v, tws, t, hook);
     fft_tail<P, p + 1>(v, lds, tws, t, hook);
@@ -565,15 +590,15 @@ __device__ __forceinline__ void fft_frame_anch(float2* v, float2* lds, float2* w
 template <class P, int p, class TW>
 __device__ __forceinline__ void fft_pair_tail(float2* a, float2* d, float2* lds, TW tws, int t) {
   // entry: LDS holds a's pass p-1 output; d finished stage p-1 in registers
-  __syncthreads();
+  plan_sync<P>();
   fft_load<P, p>(a, lds, t);
-  __syncthreads();
+  plan_sync<P>();
   fft_store<P, p - 1>(d, lds, t);
   fft_stage<P, p>(a, tws, t);
-  __syncthreads();
+  plan_sync<P>();
   fft_load<P, p>(d, lds, t);
   if constexpr (p + 1 < P::NP) {
-    __syncthreads();
+    plan_sync<P>();
     fft_store<P, p>(a, lds, t);
     fft_stage<P, p>(d, tws, t);
     fft_pair_tail<P, p + 1>(a, d, lds, tws, t);
@@ -589,7 +614,7 @@ template <class P, class TW, class H = NoHook>
 __device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW tws, int t,
                                          H hook = H{}) {
   static_assert(P::valid() && P::NP >= 2, "invalid FFT plan");
-  __syncthreads();
+  plan_sync<P>();
   fft_stage<P, 0>(a, tws, t);
   fft_store<P, 0>(a, lds, t);
   hook();

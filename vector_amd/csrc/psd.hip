@@ -333,6 +333,11 @@ hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const fl
   return hipGetLastError();
 }
 
+// Grid cap of the persistent variants (0: every resident slot).  A cap of one
+// block per CU leaves the other slot to a concurrently launched correlator.
+static int g_psd_grid_cap = 0;
+void set_psd_grid_cap(int cap) { g_psd_grid_cap = cap; }
+
 template <class PL, int PERSIST>
 void launch_psd_t(const float2* x, long long stride, const float* win, int nperseg, long long hop,
                   float scale, float* out, long long nframes, int shift, const float2* tw,
@@ -340,9 +345,11 @@ void launch_psd_t(const float2* x, long long stride, const float* win, int npers
   constexpr int BT = block_threads<PL>();
   constexpr int FPB = BT / PL::TF;
   const long long units = (nframes + FPB - 1) / FPB;
-  const long long grid =
+  long long grid =
       (PERSIST == 1 || PERSIST == 2) ? persistent_grid(psd_kernel<PL, PERSIST>, BT, units)
       : PERSIST == 6 ? (units + 1) / 2 : units;
+  if ((PERSIST == 1 || PERSIST == 2) && g_psd_grid_cap > 0 && grid > g_psd_grid_cap)
+    grid = g_psd_grid_cap;
   hipLaunchKernelGGL((psd_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(BT), 0, st, x, stride,
                      win, nperseg, hop, scale, out, nframes, shift, tw);
 }

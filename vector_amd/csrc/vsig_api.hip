@@ -32,7 +32,9 @@ struct vsig_ctx {
   std::map<std::string, TimingRec> timers;
   vsig::Variants var{64, 320, 193};       // tuned defaults (see vsig_set_option)
   int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
-  int pfb_variant = 3, pfb_fpg = 64;     // PFB: LDS-staged stores + row prefetch; frames per group
+  int pfb_variant = 3, pfb_fpg = 64;
+  int psd_grid = 0;                     // persistent PSD: grid cap (0 = all resident slots)
+  int fir_psd_variant = 0;              // bit 0: non-temporal filtered-stream stores     // PFB: LDS-staged stores + row prefetch; frames per group
 };
 
 struct vsig_fir {
@@ -360,6 +362,12 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
     (k == "fir_m" ? c->fir_m : c->xcorr_m) = value;
   } else if (k == "pfb_variant") {
     c->pfb_variant = value & 7;
+  } else if (k == "psd_grid") {
+    if (value < 0) return fail(c, VSIG_E_INVALID, "psd_grid must be >= 0");
+    c->psd_grid = value;
+    vsig::set_psd_grid_cap(value);
+  } else if (k == "fir_psd_variant") {
+    c->fir_psd_variant = value & 7;
   } else if (k == "pfb_fpg") {
     if (value < 0 || value > 65536) return fail(c, VSIG_E_INVALID, "pfb_fpg must be in [0, 65536]");
     c->pfb_fpg = value;
@@ -379,6 +387,8 @@ int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
   else if (k == "xcorr_m") *value = c->xcorr_m;
   else if (k == "pfb_variant") *value = c->pfb_variant;
   else if (k == "pfb_fpg") *value = c->pfb_fpg;
+  else if (k == "fir_psd_variant") *value = c->fir_psd_variant;
+  else if (k == "psd_grid") *value = c->psd_grid;
   else return VSIG_E_INVALID;
   return VSIG_OK;
 }
@@ -528,6 +538,30 @@ int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n,
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,
                                 f->decim, (float2*)y, tw, c->var.fir, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_fir_block(const vsig_fir* f) { return f ? f->M : 0; }
+
+int vsig_fir_psd_exec_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y,
+                          int64_t ny, const float* win, int32_t nfft, float scale, int32_t shift,
+                          float* sxx, int64_t nframes) {
+  if (!f) return VSIG_E_INVALID;
+  vsig_ctx* c = f->ctx;
+  if (!x || !y || !win || (!sxx && nframes > 0)) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
+  if (ny != n) return fail(c, VSIG_E_INVALID, "ny != n");
+  if (f->decim != 1 || f->M != 1024 || vsig::fir_psd_seg_hop(nfft) == 0 ||
+      f->ntaps - 1 + vsig::fir_psd_seg_hop(nfft) > 1024)
+    return fail(c, VSIG_E_UNSUPPORTED, "fused filter+spectrum: decim 1, nfft 8192, ntaps <= 342");
+  if (nframes != ny / nfft) return fail(c, VSIG_E_INVALID, "nframes != ny / nfft");
+  const float2 *twf, *tws;
+  int rc;
+  if ((rc = get_twiddles(c, -1024, &twf)) || (rc = get_twiddles(c, nfft, &tws))) return rc;
+  Timed t(c, "fir_psd");
+  HIPCHK(c, vsig::launch_fir_psd(nfft, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps,
+                                 (float2*)y, win, scale, shift, sxx, nframes, twf, tws,
+                                 c->fir_psd_variant, c->stream));
   return VSIG_OK;
 }
 

@@ -48,6 +48,7 @@ struct Variants { int psd, fir, xcorr; };
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
                       long long hop, float scale, float* out, long long nframes, int shift,
                       const float2* tw, int variant, hipStream_t st);
+void set_psd_grid_cap(int cap);   // persistent PSD variants: max blocks (0 = all slots)
 // Threads per frame of the spectrum plan for N points (0: no plan); the
 // anchor / pair PSD variants need >= 256 (one frame per block).
 int psd_plan_threads(int N);
@@ -57,6 +58,12 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
                           int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
                           hipStream_t st);
+// Fused FIR (M = 1024, decim 1) -> PSD (nfft = nperseg = hop = 8192), firpsd.hip.
+int fir_psd_seg_hop(int nfft);
+hipError_t launch_fir_psd(int nfft, const float2* x, long long n, long long g0, const float2* Hs,
+                          int ntaps, float2* y, const float* win, float scale, int shift,
+                          float* sxx, long long nframes, const float2* twf, const float2* tws,
+                          int variant, hipStream_t st);
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
                          int variant, hipStream_t st);

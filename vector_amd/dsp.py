@@ -237,6 +237,29 @@ class FirFilter:
                                                            _ptr(out), ny), "filter")
         return out
 
+    @property
+    def block(self) -> int:
+        """Overlap-save block size the library chose for these taps."""
+        return int(self.ctx.lib.vsig_fir_block(self.h))
+
+    def fir_psd(self, x: torch.Tensor, nhist: int, out: torch.Tensor, win: torch.Tensor,
+                nfft: int, scale: float, sxx: torch.Tensor, shift: int = 0) -> None:
+        """Fused filter + spectrum (decim 1, nfft 8192): out as __call__,
+        sxx (frame-major float32, len(out) // nfft frames) as vsig_psd_c64_dev
+        of out with nperseg = hop = nfft."""
+        self.ctx.bind_stream()
+        _check_dev(x, 1, torch.complex64, "filter input", self.ctx.device)
+        n = int(x.shape[0]) - int(nhist)
+        if n < 1 or nhist < 0:
+            raise ValueError("filter: need len(x) > nhist >= 0")
+        nframes = n // int(nfft)
+        _check_dev(out, n, torch.complex64, "filter output", self.ctx.device)
+        _check_dev(win, int(nfft), torch.float32, "window", self.ctx.device)
+        _check_dev(sxx, nframes * int(nfft), torch.float32, "spectrum output", self.ctx.device)
+        self.ctx.check(self.ctx.lib.vsig_fir_psd_exec_dev(
+            self.h, _ptr(x), int(nhist), n, _ptr(out), n, _ptr(win), int(nfft), float(scale),
+            int(shift), _ptr(sxx), nframes), "filter+spectrum")
+
     def __del__(self):
         try:
             if self.h:

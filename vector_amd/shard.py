@@ -47,6 +47,9 @@ class ChainConfig:
     pipeline: int = 1            # sub-chunks per step (FIR / PSD / xcorr overlap on 3 streams)
     serial: bool = False         # sub-chunks in order on one stream: FIR(k+1), PSD(k), xcorr(k)
                                  # (a sub-chunk's filtered samples are re-read while cache-resident)
+    fuse: bool = False           # FIR + PSD in one launch where the backend has it (decim 1,
+                                 # one sub-chunk): the PSD re-reads the filtered stream from cache
+                                 # (measured slower than two launches on MI355X: DESIGN.md §4)
 
     def validate(self, world: int):
         ny = self.n_local // self.decim
@@ -127,6 +130,14 @@ class HipBackend:
     def fir_into(self, x_ext, nhist, y):
         self.fir(x_ext, out=y, nhist=nhist)
 
+    def can_fuse(self, cfg):
+        return (cfg.decim == 1 and self.nfft == 8192 and self.fir.ntaps <= 342
+                and self.fir.block == 1024)
+
+    def fir_psd_into(self, x_ext, nhist, y, sxx):
+        """FIR (decim 1) and the PSD of its output in one launch."""
+        self.fir.fir_psd(x_ext, nhist, y, self.win, self.nfft, self.scale, sxx)
+
     def psd_into(self, y, sxx):
         ctx = self.ctx
         ctx.bind_stream()
@@ -172,6 +183,8 @@ class StreamChain:
         self.sxx = backend.empty((self.ny // cfg.nfft) * cfg.nfft, torch.float32)
         self.recs = backend.empty(4 * cfg.pipeline, torch.float64).view(cfg.pipeline, 4)
         self.peak_rows = None
+        self.fused = (cfg.fuse and cfg.pipeline == 1 and not cfg.serial and cfg.decim == 1
+                      and hasattr(backend, "fir_psd_into") and backend.can_fuse(cfg))
 
     @property
     def x(self):
@@ -202,21 +215,30 @@ class StreamChain:
         """FIR of sub-chunk 0 with the left-halo exchange hidden behind it:
         outputs from a decimation-aligned s >= ntaps-1 on need only the rank's
         own samples and are filtered while the halo is in flight; the first
-        s outputs follow once it has landed."""
+        s outputs follow once it has landed.  Fused chains (FIR + PSD in one
+        launch) split at a frame boundary s >= ntaps-1 instead."""
         r, w, hist, n = self.rank, self.world, self.hist, self.cfg.n_local
         D = self.cfg.decim
+        if self.fused:
+            nfft = self.cfg.nfft
+
+            def run(a, b):                       # outputs [a, b) (frame-aligned)
+                be.fir_psd_into(self.x_ext[a: b + hist], hist, self.y_ext[a: b], self.sxx[a: b])
+        else:
+            def run(a, b):
+                be.fir_into(self.x_ext[a: b + hist], hist, self.y_ext[a // D: b // D])
         if not (w > 1 and hist > 0):
-            be.fir_into(self.x_ext[: nk + hist], hist, self.y_ext[: nyk])
+            run(0, nk)
             return
         reqs = self._exchange_start(self.x_ext[n: n + hist] if r < w - 1 else None,
                                     r + 1 if r < w - 1 else None,
                                     self.x_ext[: hist] if r > 0 else None,
                                     r - 1 if r > 0 else None)
-        s = -(-hist // D) * D
+        s = -(-hist // nfft) * nfft if self.fused else -(-hist // D) * D
         if s < nk:
-            be.fir_into(self.x_ext[s: nk + hist], hist, self.y_ext[s // D: nyk])
+            run(s, nk)
         self._exchange_wait(reqs)
-        be.fir_into(self.x_ext[: min(s, nk) + hist], hist, self.y_ext[: min(s, nk) // D])
+        run(0, min(s, nk))
 
     def step(self):
         if self.cfg.serial:
@@ -243,9 +265,10 @@ class StreamChain:
                                    r + 1 if r < w - 1 else None)
                     ev_halo = _record(be)
         for k in range(K):
-            with _lane(be, "psd"):              # 4. PSD of sub-chunk k
-                _wait(be, ev_fir[k])
-                be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
+            if not self.fused:
+                with _lane(be, "psd"):          # 4. PSD of sub-chunk k
+                    _wait(be, ev_fir[k])
+                    be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
             if L:                               # 5. sync correlation of sub-chunk k
                 with _lane(be, "xcorr"):
                     last = k == K - 1
