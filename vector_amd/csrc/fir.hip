@@ -51,7 +51,7 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fi
   static_assert(BT == P::TF, "one frame per block");
   __shared__ float2 lds[os_lds<P, PERSIST>()];
   const int t = threadIdx.x;
-  long long b = PERSIST == 0 || PERSIST >= 3 ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  long long b = PERSIST == 0 || PERSIST >= 3 ? xcd_remap(stage_bid<1>(), gridDim.x) : blockIdx.x;
   if (b >= nblocks) return;  // uniform per block
 
   const int lo = ntaps - 1;

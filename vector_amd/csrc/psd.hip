@@ -42,7 +42,7 @@ __global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
   const long long units = (nframes + FPB - 1) / FPB;
-  long long u = blockIdx.x;
+  long long u = PERSIST == 6 ? stage_bid<2>() : blockIdx.x;
   if (u >= units) return;
   if constexpr (PERSIST == 5 || PERSIST == 6) {   // register twiddle anchors; 6: two frames (fft_pair)
     if constexpr (FPB != 1) return;                // launch_psd only picks these for TF >= 256

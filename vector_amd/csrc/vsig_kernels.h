@@ -21,6 +21,17 @@ __device__ __forceinline__ long long xcd_remap(long long b, long long nb) {
 #endif
 }
 
+// Block dispatch order of the chain's stages (A/B builds: VSIG_REV_MASK bit 0
+// FIR, bit 1 PSD, bit 2 correlator walk the stream back to front), so a stage
+// starts on the part of the stream the previous one wrote last.
+#ifndef VSIG_REV_MASK
+#define VSIG_REV_MASK 0
+#endif
+template <int STAGE>
+__device__ __forceinline__ unsigned stage_bid() {
+  return (VSIG_REV_MASK & STAGE) ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
+}
+
 enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
 
 // One block's |c| reduction partial (also the layout of the final result).

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
                 "per-element split twiddles must be 64th roots of unity");
   __shared__ float2 lds[P::LDS + (TW == 1 ? tw2_size<P>() : 0)];
   const int t = threadIdx.x;
-  const long long b = xcd_remap(blockIdx.x, gridDim.x);
+  const long long b = xcd_remap(stage_bid<4>(), gridDim.x);
   if (b >= nblocks) return;
   float2* t2 = lds + P::LDS;
   if constexpr (TW == 1) load_tw2<P>(t2, tw, t, P::TF);
