@@ -85,7 +85,9 @@ int vsig_synchronize(vsig_ctx* ctx);
  *   bit 3 LDS twiddles, bit 4 split re/im exchange, bit 5 (xcorr) partitioned
  *   template, bit 6 (xcorr, M = 16384) half-frame kernel (two blocks per CU);
  *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule;
- *   "fir_psd_variant": bit 0 non-temporal filtered-stream stores in the fused kernel.
+ *   "fir_psd_variant" (fused kernel): bit 0 non-temporal filtered-stream stores,
+ *   bit 1 block barriers in the FIR phase, bit 2 next-round segment prefetch;
+ *   "psd_grid": grid cap of the persistent PSD variants (0 = every resident slot).
  * Plans created afterwards use the new block sizes. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 /* Current value of a tuning knob (same keys as vsig_set_option). */

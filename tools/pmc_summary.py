@@ -16,7 +16,7 @@ import re
 import sys
 from collections import defaultdict
 
-FAMILY = {"fir_os_kernel": "fir", "psd_kernel": "psd", "xcorr_os_kernel": "xcorr",
+FAMILY = {"fir_psd_kernel": "fir_psd", "fir_os_kernel": "fir", "psd_kernel": "psd", "xcorr_os_kernel": "xcorr",
           "xcorr_part_kernel": "xcorr", "xcorr_half_kernel": "xcorr", "pfb_kernel": "pfb",
           "peak_reduce": "peak", "partial_finalize": "finalize"}
 

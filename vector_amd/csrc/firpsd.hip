@@ -159,17 +159,17 @@ hipError_t launch_fir_psd(int nfft, const float2* x, long long n, long long g0, 
   if ((nframes + 1) / 2 > nblocks) return hipErrorInvalidValue;
   const dim3 g((unsigned)nblocks), b(PS::TF);
   // variant bit 0: non-temporal y stores; bit 1: block barriers in the FIR
-  // phase (instead of wave barriers); bit 2: no next-round prefetch
+  // phase (instead of wave barriers); bit 2: next-round prefetch (spills)
 #define VSIG_FP(NT, PF_, PREF)                                                                  \
   hipLaunchKernelGGL((fir_psd_kernel<PF_, PS, ROUNDS, NT, PREF>), g, b, 0, st, x, n, g0, Hs,    \
                      ntaps, sh, y, win, scale, shift, sxx, nframes, nblocks, twf, tws)
   using PW = WaveSync<Plan1024s>;
   switch (variant & 7) {
-    case 0: VSIG_FP(false, PW, true); break;
-    case 1: VSIG_FP(true, PW, true); break;
-    case 2: VSIG_FP(false, Plan1024s, true); break;
-    case 4: VSIG_FP(false, PW, false); break;
-    case 6: VSIG_FP(false, Plan1024s, false); break;
+    case 0: VSIG_FP(false, PW, false); break;
+    case 1: VSIG_FP(true, PW, false); break;
+    case 2: VSIG_FP(false, Plan1024s, false); break;
+    case 4: VSIG_FP(false, PW, true); break;
+    case 6: VSIG_FP(false, Plan1024s, true); break;
     default: return hipErrorInvalidValue;
   }
 #undef VSIG_FP
