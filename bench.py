@@ -136,6 +136,9 @@ def main():
                     help="run the --pipeline sub-chunks in order on one stream (cache reuse)")
     for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m", "fir_psd_variant", "psd_grid"):
         ap.add_argument("--" + k.replace("_", "-"), type=int, default=None)
+    ap.add_argument("--freq-shift", type=float, default=0.0,
+                    help="NCO mixer (apply_frequency_shift) fused into the FIR loads, Hz")
+    ap.add_argument("--sample-rate", type=float, default=2e9, help="for --freq-shift (config 5: 2 GS/s)")
     ap.add_argument("--fuse", action="store_true",
                     help="FIR and PSD in one fused launch (D=1, nfft 8192; default: two launches)")
     ap.add_argument("--workload", choices=("chain", "pfb"), default="chain",
@@ -171,7 +174,8 @@ def main():
         if v is not None:
             ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, k.encode(), v), k)
     cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl,
-                      pipeline=args.pipeline, serial=args.serial, fuse=args.fuse)
+                      pipeline=args.pipeline, serial=args.serial, fuse=args.fuse,
+                      freq_shift=args.freq_shift, sample_rate=args.sample_rate)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)
     N = world * n
@@ -286,7 +290,8 @@ def main():
                    "samples_per_gpu": n, "total_samples": N, "ntaps": args.ntaps,
                    "decim": args.decim, "nfft": args.nfft, "template": args.template,
                    "parallelism": f"time-chunk x{world} (RCCL halos)",
-                   "pipeline": args.pipeline, "serial": args.serial, "fused": chain.fused},
+                   "pipeline": args.pipeline, "serial": args.serial, "fused": chain.fused,
+                   "freq_shift": args.freq_shift},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},

@@ -23,8 +23,12 @@ class OracleBackend:
     def empty(self, n, dtype=torch.complex64):
         return torch.zeros(n, dtype=dtype)
 
-    def fir_into(self, x_ext, nhist, y):
+    def fir_into(self, x_ext, nhist, y, i0=None):
         x = x_ext.contiguous().numpy()
+        if self.cfg.freq_shift:          # apply_frequency_shift at global indices i0 + k
+            assert i0 is not None
+            t = (i0 + np.arange(len(x))) / self.cfg.sample_rate
+            x = (x * np.exp(2j * np.pi * self.cfg.freq_shift * t)).astype(np.complex64)
         full = np.convolve(x, self.cfg.taps)[nhist: len(x)]
         y.copy_(torch.from_numpy(full[:: self.cfg.decim].astype(np.complex64)))
 
@@ -41,7 +45,10 @@ class OracleBackend:
         rec.view(torch.int64)[1] = i
 
 
-def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
+FS, SR = 0.0137, 1.0    # mixer of the freq_shift cases (cycles per sample)
+
+
+def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None, freq_shift=0.0):
     rng = np.random.default_rng(world)
     N = world * n_local
     x = ref.synth_iq(N, seed=world)
@@ -49,27 +56,30 @@ def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None):
     pre = ref.qpsk_preamble(L, seed=7)
     if k0 is None:   # straddles the first rank boundary (or a sub-chunk boundary on 1 rank)
         k0 = n_local // decim - L // 2 if world > 1 else n_local // decim // 4 - L // 2
-    y_full = np.convolve(x, taps)[:N][::decim].astype(np.complex64)
+    xm = ref.apply_frequency_shift(x, freq_shift, SR) if freq_shift else x
+    y_full = np.convolve(xm, taps)[:N][::decim].astype(np.complex64)
     y_full[k0:k0 + L] += 6 * pre                                   # plant after filtering
     return x, taps, pre, k0, y_full
 
 
 def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, serial=False,
-            fuse=False):
+            fuse=False, freq_shift=0.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from vector_amd.shard import ChainConfig, StreamChain
-        x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L)
+        x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L,
+                                        freq_shift=freq_shift)
         cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre,
-                          pipeline=pipeline, serial=serial, fuse=fuse)
+                          pipeline=pipeline, serial=serial, fuse=fuse, freq_shift=freq_shift,
+                          sample_rate=SR)
         be = OracleBackend(cfg)
 
         class PlantingBackend(OracleBackend):
             """Adds the preamble to the filtered stream at global k0 (as the
             single-stream reference does) before the PSD / xcorr stages."""
-            def fir_into(self, x_ext, nhist, y):
-                super().fir_into(x_ext, nhist, y)
+            def fir_into(self, x_ext, nhist, y, i0=None):
+                super().fir_into(x_ext, nhist, y, i0)
                 nyk = y.shape[0]
                 start = (y.data_ptr() - ch_holder[0].y_ext.data_ptr()) // 8   # sub-chunk offset
                 lo = rank * (n_local // decim) + start
@@ -106,20 +116,22 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,pipeline,serial,fuse", [
-    (2, 1, False, False), (3, 1, False, False), (2, 4, False, False), (1, 4, False, False),
-    (2, 4, True, False), (3, 2, True, False), (2, 1, False, True), (3, 1, False, True),
-    (1, 1, False, True)])
-def test_sharded_chain_matches_single_stream(world, pipeline, serial, fuse):
+@pytest.mark.parametrize("world,pipeline,serial,fuse,freq_shift", [
+    (2, 1, False, False, 0.0), (3, 1, False, False, 0.0), (2, 4, False, False, 0.0),
+    (1, 4, False, False, 0.0), (2, 4, True, False, 0.0), (3, 2, True, False, 0.0),
+    (2, 1, False, True, 0.0), (3, 1, False, True, 0.0), (1, 1, False, True, 0.0),
+    (3, 1, False, False, FS), (2, 4, True, False, FS)])
+def test_sharded_chain_matches_single_stream(world, pipeline, serial, fuse, freq_shift):
     """fuse: the fused FIR + PSD launch (decim 1), split at a frame boundary on
-    ranks > 0 so the bulk runs while the left halo is in flight."""
+    ranks > 0 so the bulk runs while the left halo is in flight.  freq_shift:
+    the mixer before the FIR, phase from the global sample index on every rank."""
     n_local, decim, nfft, ntaps, L = 4096, 1 if fuse else 2, 256, 31, 100
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_worker,
                          args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline, serial,
-                               fuse))
+                               fuse, freq_shift))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -130,7 +142,8 @@ def test_sharded_chain_matches_single_stream(world, pipeline, serial, fuse):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    x, taps, pre, k0, y_full = make_case(world, n_local, decim, nfft, ntaps, L)
+    x, taps, pre, k0, y_full = make_case(world, n_local, decim, nfft, ntaps, L,
+                                         freq_shift=freq_shift)
     ny = n_local // decim
     y_cat = np.concatenate([res[r][0] for r in range(world)])
     np.testing.assert_allclose(y_cat, y_full, rtol=0, atol=1e-5 * np.abs(y_full).max())

@@ -59,6 +59,7 @@ SIGNATURES = {
     "vsig_fir_exec_hist_dev": (C.c_int, [P, P, I64, I64, P, I64]),
     "vsig_fir_c64": (C.c_int, [P, P, I64, P, I32, I32, P, I64]),
     "vsig_fir_block": (C.c_int, [P]),
+    "vsig_fir_exec_mix_dev": (C.c_int, [P, P, I64, I64, P, I64, C.c_double, C.c_double, I64]),
     "vsig_fir_psd_exec_dev": (C.c_int, [P, P, I64, I64, P, I64, P, I32, F32, I32, P, I64]),
     "vsig_xcorr_create": (C.c_int, [P, P, I32, C.POINTER(P)]),
     "vsig_xcorr_free": (None, [P]),

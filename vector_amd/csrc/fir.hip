@@ -41,11 +41,12 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 // The segment x[b*hop - (ntaps-1) .. + M) is FFT'd, multiplied by Hs = FFT(h)/M
 // and inverse-transformed (conj trick), all in LDS / registers.
 // ---------------------------------------------------------------------------
-template <class P, int PERSIST>
+template <class P, int PERSIST, bool MIX = false>
 __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
-    const float2* __restrict__ tw) {
+    const float2* __restrict__ tw, MixArgs mix) {
+  static_assert(!MIX || PERSIST == 6, "the fused mixer is built for the pair kernel");
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   constexpr int BT = os_threads<P>();
   static_assert(BT == P::TF, "one frame per block");
@@ -76,8 +77,13 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fi
     else load_anchors<P>(wa, tw, t);
     const long long b0 = 2 * b, b1 = 2 * b + 1;
     float2 a[P::E], d[P::E];
-    load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
-    load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
+    if constexpr (MIX) {
+      load_segment_mix<P>(a, x, g0 + b0 * hop - lo, n, t, mix);
+      load_segment_mix<P>(d, x, g0 + b1 * hop - lo, n, t, mix);
+    } else {
+      load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
+      load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
+    }
     auto fft2 = [&]() {
       if constexpr (RT) fft_pair<P>(a, d, lds, TwRegs{wa}, t);
       else { launder_anchors<P>(wa); fft_pair<P>(a, d, lds, TwAnchors{wa}, t); }
@@ -177,11 +183,11 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fi
 // is a multiple of D.  Two segments per wave (fft_pair), anchors for the
 // M-point transforms, exact register twiddles for the small ones.
 // ---------------------------------------------------------------------------
-template <class P, class PD>
+template <class P, class PD, bool MIX = false>
 __global__ __launch_bounds__(P::TF) void fir_dec_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs, int lo2,
     long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
-    const float2* __restrict__ twd) {
+    const float2* __restrict__ twd, MixArgs mix) {
   constexpr int D = P::N / PD::N;
   static_assert(P::TF == PD::TF && P::E == D * PD::E && P::RL == P::E && PD::R[0] == PD::E,
                 "fold needs thread t to hold bins t + TF r of both plans");
@@ -195,8 +201,13 @@ __global__ __launch_bounds__(P::TF) void fir_dec_kernel(
   float2 wr[rtw_total<PD>()];
   load_rtw<PD>(wr, twd, t);
   float2 a[P::E], d[P::E];
-  load_segment<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
-  load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
+  if constexpr (MIX) {
+    load_segment_mix<P>(a, x, g0 + (2 * b) * hop - lo2, n, t, mix);
+    load_segment_mix<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t, mix);
+  } else {
+    load_segment<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
+    load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
+  }
   launder_anchors<P>(wa);
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
   float2 ua[PD::E], ud[PD::E];
@@ -231,36 +242,51 @@ __global__ __launch_bounds__(P::TF) void fir_dec_kernel(
 
 hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
                           int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
-                          hipStream_t st) {
+                          hipStream_t st, const MixArgs* mix) {
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
   const dim3 g((unsigned)((nblocks + 1) / 2)), blk(Plan1024s::TF);
-  if (decim == 4)
-    hipLaunchKernelGGL((fir_dec_kernel<Plan1024s, Plan256d>), g, blk, 0, st, x, n, g0, Hs, lo2, hop, y, nblocks, tw, twd);
-  else if (decim == 2)
-    hipLaunchKernelGGL((fir_dec_kernel<Plan1024s, Plan512d>), g, blk, 0, st, x, n, g0, Hs, lo2, hop, y, nblocks, tw, twd);
-  else
-    return hipErrorInvalidValue;
+  const MixArgs m = mix ? *mix : MixArgs{0.0, 1.0, 0};
+#define VSIG_FD(PD)                                                                              \
+  do {                                                                                           \
+    if (mix)                                                                                     \
+      hipLaunchKernelGGL((fir_dec_kernel<Plan1024s, PD, true>), g, blk, 0, st, x, n, g0, Hs, lo2, \
+                         hop, y, nblocks, tw, twd, m);                                           \
+    else                                                                                         \
+      hipLaunchKernelGGL((fir_dec_kernel<Plan1024s, PD, false>), g, blk, 0, st, x, n, g0, Hs,    \
+                         lo2, hop, y, nblocks, tw, twd, m);                                      \
+  } while (0)
+  if (decim == 4) VSIG_FD(Plan256d);
+  else if (decim == 2) VSIG_FD(Plan512d);
+  else return hipErrorInvalidValue;
+#undef VSIG_FD
   return hipGetLastError();
 }
 
-template <class PL, int PERSIST>
+template <class PL, int PERSIST, bool MIX = false>
 void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, int ntaps,
                   long long hop, int decim, float2* y, long long nblocks, const float2* tw,
-                  hipStream_t st) {
+                  hipStream_t st, MixArgs mix = MixArgs{0.0, 1.0, 0}) {
   const long long grid =
       (PERSIST == 1 || PERSIST == 2)
           ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks)
           : (PERSIST == 6 || PERSIST == 7) ? (nblocks + 1) / 2 : nblocks;
-  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(os_threads<PL>()),
-                     0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw);
+  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST, MIX>), dim3((unsigned)grid), dim3(os_threads<PL>()),
+                     0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, mix);
 }
 
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
-                         int variant, hipStream_t st) {
+                         int variant, hipStream_t st, const MixArgs* mix) {
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
+  if (mix) {   // fused mixer: the default pair kernel (register anchors) only
+    if ((variant & (8 | 16 | 128)) || !(variant & 64)) return hipErrorInvalidValue;
+    VSIG_OS_SWITCH(M, variant, {
+      launch_fir_t<PL, 6, true>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st, *mix);
+    });
+    return hipGetLastError();
+  }
   VSIG_OS_SWITCH(M, variant, {
     // (bits 3/4 first: they select the two-level twiddle table the API built)
     if (variant & 16) launch_fir_t<PL, 4>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);

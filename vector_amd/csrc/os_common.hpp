@@ -73,6 +73,17 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
   }
 }
 
+// load_segment with the NCO mixer applied to each sample (global index
+// mix.i0 + s0 + i; the zero fill stays zero).
+template <class P>
+__device__ __forceinline__ void load_segment_mix(float2* v, const float2* __restrict__ x,
+                                                 long long s0, long long n, int t, const MixArgs& mix) {
+  load_segment<P>(v, x, s0, n, t);
+  const long long g = mix.i0 + s0;
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) v[e] = mix_at(v[e], g + in_index<P>(t, e), mix.w, mix.sr);
+}
+
 // ---------------------------------------------------------------------------
 // Block partial of a |c| reduction: max |c|^2 (lowest index on ties),
 // sum |c|, sum |c|^2.

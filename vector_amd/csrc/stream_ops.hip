@@ -27,21 +27,9 @@ static int ew_grid(long long n) {
 // ---------------------------------------------------------------- mixer
 __global__ __launch_bounds__(256) void mix_c64(const float2* __restrict__ x, long long n, double w,
                                                double sr, long long i0, float2* __restrict__ y) {
-  // 2*pi split for a Cody-Waite reduction of theta = w * t (|theta| < 2^40 or so)
-  constexpr double kTwoPiHi = 6.28318530717958623200e+00;
-  constexpr double kTwoPiLo = 2.44929359829470635445e-16;
-  constexpr double kInvTwoPi = 1.59154943091895345608e-01;
   const long long stride = (long long)gridDim.x * 256;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const double t = __ddiv_rn((double)(i0 + i), sr);   // np.arange(n) / sample_rate
-    const double th = __dmul_rn(w, t);                   // (2j*pi*f) * t, imaginary part
-    const double k = rint(th * kInvTwoPi);
-    const double r = fma(-k, kTwoPiLo, fma(-k, kTwoPiHi, th));
-    float s, c;
-    sincosf((float)r, &s, &c);
-    const float2 v = x[i];
-    y[i] = make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
-  }
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
+    y[i] = mix_at(x[i], i0 + i, w, sr);
 }
 
 // ---------------------------------------------------------------- scale

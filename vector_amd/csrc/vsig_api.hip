@@ -511,8 +511,8 @@ void vsig_fir_free(vsig_fir* f) {
   delete f;
 }
 
-int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y,
-                           int64_t ny) {
+static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y, int64_t ny,
+                    const vsig::MixArgs* mix) {
   if (!f) return VSIG_E_INVALID;
   vsig_ctx* c = f->ctx;
   if (!x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
@@ -530,14 +530,16 @@ int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n,
     if (hop < D) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
     Timed t(c, "fir");
     HIPCHK(c, vsig::launch_fir_dec(D, (const float2*)x, nhist + n, nhist, f->Hs, lo2, hop, (float2*)y,
-                                   tw, twd, c->stream));
+                                   tw, twd, c->stream, mix));
     return VSIG_OK;
   }
+  if (mix && ((c->var.fir & (8 | 16 | 128)) || !(c->var.fir & 64)))
+    return fail(c, VSIG_E_UNSUPPORTED, "fused mixer needs the default FIR variant");
   rc = get_tw_for(c, f->M, c->var.fir, true, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,
-                                f->decim, (float2*)y, tw, c->var.fir, c->stream));
+                                f->decim, (float2*)y, tw, c->var.fir, c->stream, mix));
   return VSIG_OK;
 }
 
@@ -563,6 +565,20 @@ int vsig_fir_psd_exec_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, 
                                  (float2*)y, win, scale, shift, sxx, nframes, twf, tws,
                                  c->fir_psd_variant, c->stream));
   return VSIG_OK;
+}
+
+int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y,
+                           int64_t ny) {
+  return fir_exec(f, x, nhist, n, y, ny, nullptr);
+}
+
+int vsig_fir_exec_mix_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y, int64_t ny,
+                          double freq_shift, double sample_rate, int64_t i0) {
+  if (!f) return VSIG_E_INVALID;
+  if (freq_shift == 0.0) return fir_exec(f, x, nhist, n, y, ny, nullptr);   // utils.py:122-123
+  if (!(sample_rate != 0.0)) return fail(f->ctx, VSIG_E_INVALID, "sample_rate must be non-zero");
+  const vsig::MixArgs m{(2.0 * M_PI) * freq_shift, sample_rate, (long long)i0};
+  return fir_exec(f, x, nhist, n, y, ny, &m);
 }
 
 int vsig_fir_exec_dev(vsig_fir* f, const void* x, int64_t n, void* y, int64_t ny) {

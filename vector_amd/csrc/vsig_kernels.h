@@ -34,6 +34,28 @@ __device__ __forceinline__ unsigned stage_bid() {
 
 enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
 
+// NCO mixer of apply_frequency_shift (utils.py:120-127): x[gi] * exp(j theta),
+// theta = w * (gi / sr) with w = (2 pi) f, formed in double exactly as numpy
+// forms it (t = np.arange(n) / sample_rate; (2j*pi*f) * t), reduced modulo 2 pi
+// in double (Cody-Waite), rotation in fp32.  Used by mix_c64 and fused into the
+// FIR's segment loads (fir.hip).
+struct MixArgs {
+  double w, sr;
+  long long i0;      // global sample index of x[0]
+};
+__device__ __forceinline__ float2 mix_at(float2 v, long long gi, double w, double sr) {
+  constexpr double kTwoPiHi = 6.28318530717958623200e+00;
+  constexpr double kTwoPiLo = 2.44929359829470635445e-16;
+  constexpr double kInvTwoPi = 1.59154943091895345608e-01;
+  const double t = __ddiv_rn((double)gi, sr);          // np.arange(n) / sample_rate
+  const double th = __dmul_rn(w, t);                   // imaginary part of (2j*pi*f) * t
+  const double k = rint(th * kInvTwoPi);
+  const double r = fma(-k, kTwoPiLo, fma(-k, kTwoPiHi, th));
+  float s, c;
+  sincosf((float)r, &s, &c);
+  return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+}
+
 // One block's |c| reduction partial (also the layout of the final result).
 struct PeakPartial {
   double max2;       // max |c|^2 (kernels on |c|^2) or max |c| (peak_reduce / finalized)
@@ -66,9 +88,10 @@ int psd_plan_threads(int N);
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
                                 const float2* tw, hipStream_t st);
 // Decimating FIR in the frequency domain (M = 1024, D = 2 / 4; see fir.hip).
+// mix != nullptr: the mixer above applied to every loaded sample (fused).
 hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
                           int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
-                          hipStream_t st);
+                          hipStream_t st, const MixArgs* mix = nullptr);
 // Fused FIR (M = 1024, decim 1) -> PSD (nfft = nperseg = hop = 8192), firpsd.hip.
 int fir_psd_seg_hop(int nfft);
 hipError_t launch_fir_psd(int nfft, const float2* x, long long n, long long g0, const float2* Hs,
@@ -77,7 +100,7 @@ hipError_t launch_fir_psd(int nfft, const float2* x, long long n, long long g0, 
                           int variant, hipStream_t st);
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
-                         int variant, hipStream_t st);
+                         int variant, hipStream_t st, const MixArgs* mix = nullptr);
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, const float2* wt,

@@ -220,10 +220,13 @@ class FirFilter:
         return (n + self.decim - 1) // self.decim
 
     def __call__(self, x: torch.Tensor, out: torch.Tensor | None = None,
-                 nhist: int = 0) -> torch.Tensor:
+                 nhist: int = 0, freq_shift: float = 0.0, sample_rate: float = 1.0,
+                 i0: int = 0) -> torch.Tensor:
         """x: 1-D complex64 CUDA tensor -> complex64 CUDA tensor (async).
         The first nhist samples of x are history (a left halo): only the
-        remaining samples produce outputs."""
+        remaining samples produce outputs.  freq_shift != 0 filters
+        apply_frequency_shift(x, freq_shift, sample_rate) instead (the NCO
+        mixer fused into the filter's loads; x[0] is global sample i0)."""
         self.ctx.bind_stream()
         _check_dev(x, 1, torch.complex64, "filter input", self.ctx.device)
         n = int(x.shape[0]) - int(nhist)
@@ -233,8 +236,13 @@ class FirFilter:
         if out is None:
             out = torch.empty(ny, dtype=torch.complex64, device=x.device)
         _check_dev(out, ny, torch.complex64, "filter output", self.ctx.device)
-        self.ctx.check(self.ctx.lib.vsig_fir_exec_hist_dev(self.h, _ptr(x), int(nhist), n,
-                                                           _ptr(out), ny), "filter")
+        if freq_shift:
+            self.ctx.check(self.ctx.lib.vsig_fir_exec_mix_dev(
+                self.h, _ptr(x), int(nhist), n, _ptr(out), ny, float(freq_shift),
+                float(sample_rate), int(i0)), "filter (mixed)")
+        else:
+            self.ctx.check(self.ctx.lib.vsig_fir_exec_hist_dev(self.h, _ptr(x), int(nhist), n,
+                                                               _ptr(out), ny), "filter")
         return out
 
     @property
@@ -285,9 +293,13 @@ def _cached_fir(taps_c64: np.ndarray, decim: int, device: int) -> FirFilter:
     return f
 
 
-def fir_filter(x, taps, decim: int = 1):
+def fir_filter(x, taps, decim: int = 1, freq_shift: float = 0.0, sample_rate: float = 1.0):
     """Causal FIR then stride decimation: ``np.convolve(x, taps, 'full')[:len(x)][::decim]``
-    (the reference's idioms, utils.py:802,816 and utils.py:194)."""
+    (the reference's idioms, utils.py:802,816 and utils.py:194).  With
+    ``freq_shift`` the input is first mixed as ``apply_frequency_shift(x,
+    freq_shift, sample_rate)`` (utils.py:120-127) inside the same kernel."""
+    if freq_shift and float(sample_rate) == 0.0:
+        raise ZeroDivisionError("float division by zero")
     taps_np = np.asarray(taps)
     if taps_np.size == 0:
         raise ValueError("v cannot be empty")
@@ -297,7 +309,7 @@ def fir_filter(x, taps, decim: int = 1):
     ctx = _lib.get_context()
     f = _cached_fir(np.ascontiguousarray(taps_np.ravel(), dtype=np.complex64), int(decim), ctx.device)
     xd = _device_c64(x, ctx)
-    y = f(xd)
+    y = f(xd, freq_shift=freq_shift, sample_rate=sample_rate)
     if _is_dev(x):
         return y
     xa = np.asarray(x)

@@ -47,6 +47,8 @@ class ChainConfig:
     pipeline: int = 1            # sub-chunks per step (FIR / PSD / xcorr overlap on 3 streams)
     serial: bool = False         # sub-chunks in order on one stream: FIR(k+1), PSD(k), xcorr(k)
                                  # (a sub-chunk's filtered samples are re-read while cache-resident)
+    freq_shift: float = 0.0      # apply_frequency_shift before the FIR (fused into its loads),
+    sample_rate: float = 1.0     # phase from the global sample index (utils.py:120-127)
     fuse: bool = False           # FIR + PSD in one launch where the backend has it (decim 1,
                                  # one sub-chunk): the PSD re-reads the filtered stream from cache
                                  # (measured slower than two launches on MI355X: DESIGN.md §4)
@@ -98,6 +100,7 @@ class HipBackend:
         self.win = torch.from_numpy(w).to(self.dev)
         self.scale = float(1.0 / float(np.sum(w, dtype=np.float64)) ** 2)
         self.nfft = cfg.nfft
+        self.freq_shift, self.sample_rate = cfg.freq_shift, cfg.sample_rate
         self.lanes = {k: torch.cuda.Stream(device=self.dev) for k in ("fir", "psd", "xcorr")}
 
     def empty(self, n, dtype=torch.complex64):
@@ -127,11 +130,13 @@ class HipBackend:
         for st in self.lanes.values():
             st.wait_stream(cur)
 
-    def fir_into(self, x_ext, nhist, y):
-        self.fir(x_ext, out=y, nhist=nhist)
+    def fir_into(self, x_ext, nhist, y, i0=0):
+        """i0: global sample index of x_ext[0] (the mixer's phase origin)."""
+        self.fir(x_ext, out=y, nhist=nhist, freq_shift=self.freq_shift,
+                 sample_rate=self.sample_rate, i0=i0)
 
     def can_fuse(self, cfg):
-        return (cfg.decim == 1 and self.nfft == 8192 and self.fir.ntaps <= 342
+        return (cfg.decim == 1 and not cfg.freq_shift and self.nfft == 8192 and self.fir.ntaps <= 342
                 and self.fir.block == 1024)
 
     def fir_psd_into(self, x_ext, nhist, y, sxx):
@@ -211,6 +216,14 @@ class StreamChain:
     def _exchange(self, send, dst, recv, src):
         self._exchange_wait(self._exchange_start(send, dst, recv, src))
 
+    def _fir(self, be, a, b, y):
+        """FIR of the rank's input samples [a, b) (plus their history) into y."""
+        x = self.x_ext[a: b + self.hist]
+        if self.cfg.freq_shift:
+            be.fir_into(x, self.hist, y, self.rank * self.cfg.n_local - self.hist + a)
+        else:
+            be.fir_into(x, self.hist, y)
+
     def _fir_first(self, be, nk, nyk):
         """FIR of sub-chunk 0 with the left-halo exchange hidden behind it:
         outputs from a decimation-aligned s >= ntaps-1 on need only the rank's
@@ -226,7 +239,7 @@ class StreamChain:
                 be.fir_psd_into(self.x_ext[a: b + hist], hist, self.y_ext[a: b], self.sxx[a: b])
         else:
             def run(a, b):
-                be.fir_into(self.x_ext[a: b + hist], hist, self.y_ext[a // D: b // D])
+                self._fir(be, a, b, self.y_ext[a // D: b // D])
         if not (w > 1 and hist > 0):
             run(0, nk)
             return
@@ -255,8 +268,7 @@ class StreamChain:
                 if k == 0:
                     self._fir_first(be, nk, nyk)
                 else:
-                    be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
-                                self.y_ext[k * nyk: (k + 1) * nyk])
+                    self._fir(be, k * nk, (k + 1) * nk, self.y_ext[k * nyk: (k + 1) * nyk])
                 ev_fir.append(_record(be))
                 if k == 0 and w > 1 and L > 1:  # 3. right halo of the filtered stream
                     self._exchange(self.y_ext[: L - 1] if r > 0 else None,
@@ -301,8 +313,7 @@ class StreamChain:
             if k == 0:                          # with the left-halo exchange
                 self._fir_first(be, nk, nyk)
                 return
-            be.fir_into(self.x_ext[k * nk: (k + 1) * nk + hist], hist,
-                        self.y_ext[k * nyk: (k + 1) * nyk])
+            self._fir(be, k * nk, (k + 1) * nk, self.y_ext[k * nyk: (k + 1) * nyk])
 
         def consume(k):
             be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
