@@ -13,6 +13,8 @@ correlation halos and 32-byte peak records over RCCL.
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
   python bench.py --workload pfb      # BASELINE config 4 (64-channel PFB), not the headline
+  python bench.py --workload sync     # BASELINE config 3 (4096-sample preamble over 2**30)
+  python bench.py --freq-shift 3e8    # the chain with the NCO mixer fused into the FIR
 
 
 Inputs are generated on the device before timing (data resident in HBM).
@@ -141,8 +143,9 @@ def main():
     ap.add_argument("--sample-rate", type=float, default=2e9, help="for --freq-shift (config 5: 2 GS/s)")
     ap.add_argument("--fuse", action="store_true",
                     help="FIR and PSD in one fused launch (D=1, nfft 8192; default: two launches)")
-    ap.add_argument("--workload", choices=("chain", "pfb"), default="chain",
-                    help="chain: the headline FIR->PSD->xcorr metric; pfb: config 4 channelizer")
+    ap.add_argument("--workload", choices=("chain", "pfb", "sync"), default="chain",
+                    help="chain: the headline FIR->PSD->xcorr metric; pfb: config 4 channelizer; "
+                         "sync: config 3 preamble correlation over 2**30 samples")
     ap.add_argument("--nchan", type=int, default=64)
     ap.add_argument("--branch-taps", type=int, default=16)
     ap.add_argument("--pfb-variant", type=int, default=None)
@@ -163,6 +166,8 @@ def main():
     import vector_amd  # noqa: F401
     if args.workload == "pfb":
         return run_pfb(args, world, rank, local, dev)
+    if args.workload == "sync":
+        return run_sync(args, world, rank, local, dev)
     from vector_amd.shard import ChainConfig, HipBackend, StreamChain
 
     n = args.samples
@@ -181,6 +186,9 @@ def main():
     N = world * n
     ny_total = N // args.decim
     k0 = (ny_total // 2 + 12_345) * args.decim     # global input sample of the preamble
+    if args.freq_shift:   # plant the preamble so that it leaves the mixer unrotated
+        ph = 2 * np.pi * args.freq_shift * ((k0 + np.arange(len(pre))) / args.sample_rate)
+        pre = (pre * np.exp(-1j * ph)).astype(np.complex64)
     generate_chunk(chain.x, rank * n, 20250718 + rank, pre, k0)
     torch.cuda.synchronize()
 
@@ -301,6 +309,94 @@ def main():
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def run_sync(args, world, rank, local, dev):
+    """BASELINE config 3: a 4096-sample QPSK preamble (SURVEY.md §8(d):
+    default_rng(4096)) slid over a 2**30-sample synthetic stream planted at
+    k0 = 123 456 789; valid correlation with the fused |c| argmax / sums
+    (correlate_peak: cross_correlate_signals + find_correlation_peak,
+    utils.py:1258-1342) on one GPU.  A step = one correlator launch + its
+    partial finalize over the device-resident stream."""
+    import ctypes as C
+    from vector_amd import dsp
+    if world != 1:
+        raise SystemExit("--workload sync is BASELINE config 3 (one GPU)")
+    n = args.samples if args.samples != 1 << 28 else 1 << 30
+    L = args.template
+    from oracle import ref            # preamble generator (same seed as the oracle's goldens)
+    pre = ref.qpsk_preamble(L, seed=4096)
+    k0 = 123_456_789 if n > 123_456_789 + L else n // 3
+    x = torch.empty(n, dtype=torch.complex64, device=dev)
+    generate_chunk(x, 0, 20250718, pre, k0)
+    xc = dsp.Correlator(pre, local)
+    pk = torch.zeros(4, dtype=torch.float64, device=dev)
+    torch.cuda.synchronize()
+    for _ in range(args.warmup):
+        xc(x, "valid", peak=pk)
+    torch.cuda.synchronize()
+    lib, h = xc.ctx.lib, xc.ctx.h
+    lib.vsig_timing_reset(h)
+    lib.vsig_timing_enable(h, 0 if args.no_kernel_timing else 1)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        xc(x, "valid", peak=pk)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    lib.vsig_timing_enable(h, 0)
+    peak, idx, s1, s2 = dsp._read_peak(pk)
+    nout = n - L + 1
+    conf = dsp._confidence(peak, s1, s2, nout, 0.5)
+    tot, cnt = C.c_double(), C.c_int64()
+    lib.vsig_timing_read(h, b"xcorr", C.byref(tot), C.byref(cnt))
+    roof = None
+    stage = {}
+    if cnt.value:
+        ms = tot.value / cnt.value
+        nbytes = 8 * n
+        ach = nbytes / (ms * 1e-3) / 1e9
+        M = xcorr_block(L, args.xcorr_m)
+        nb = -(-nout // (M - L + 1))
+        flops = nb * (2 * 5 * M * np.log2(M) + 6 * M)
+        tf = flops / (ms * 1e-3) / 1e12
+        pmc = load_traffic(f"xcorr:n={n}:L={L}")
+        roof = {"bound": "hbm", "kernel": "xcorr", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
+                "traffic_source": pmc["source"] if pmc else None}
+        stage = {"xcorr": {"ms": round(ms, 4), "TFLOPs": round(tf, 2),
+                           "valu_peak_TFLOPs": FP32_PEAK_TF, "valu_frac": round(tf / FP32_PEAK_TF, 4),
+                           "M": M}}
+    cpu = None
+    if not args.no_cpu_baseline:
+        ns = 1 << 21
+        xs = ref.synth_iq(ns, seed=99)
+        t1 = time.perf_counter()
+        c, lags = ref.cross_correlate_signals(pre, xs, "valid")
+        ref.find_correlation_peak(c, lags)
+        dt = time.perf_counter() - t1
+        cpu = dict(value=round(ns / dt / 1e6, 3), unit="Msamples/s", cores=1, kind="port",
+                   sample=(f"{ns} samples (2**21) through np.correlate complex128 L={L} valid + "
+                           f"find_correlation_peak, {dt:.2f} s, 1 thread (direct O(N L); the "
+                           f"full 2**30 stream would take ~{n / (ns / dt) / 60:.0f} min)"),
+                   seconds=round(dt, 3), cores_available=len(os.sched_getaffinity(0)))
+    out = {
+        "metric": "Msamples/s c64 through the sliding-correlation sync (BASELINE config 3)",
+        "value": round(n / (elapsed / args.steps) / 1e6, 1), "unit": "Msamples/s",
+        "n_gpus": 1, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "c64 (fp32)",
+        "data": "synthetic IQ generated on device: 3 tones + CN(0,1) noise + QPSK preamble",
+        "config": {"workload": (f"BASELINE configs[2]: {L}-sample preamble over a {n}-sample "
+                                f"c64 stream, valid correlation + argmax detect"),
+                   "samples": n, "template": L, "parallelism": "1 GPU"},
+        "roofline": roof, "cpu_baseline": cpu, "stages_roofline": stage,
+        "check": {"lag": idx, "expected": k0, "ok": bool(idx == k0), "peak": round(peak, 3),
+                  "confidence": round(conf, 4)},
+    }
+    print(json.dumps(out), flush=True)
 
 
 def run_pfb(args, world, rank, local, dev):

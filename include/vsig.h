@@ -137,7 +137,8 @@ int vsig_fir_exec_hist_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t 
  * fused into the FIR's loads: filters x[i] * exp(2j*pi*freq_shift*t_i),
  * t_i = (i0 + i) / sample_rate, i0 = global sample index of x[0] (the first
  * history sample), i.e. vsig_mix_c64_dev then vsig_fir_exec_hist_dev in one
- * pass.  freq_shift == 0: plain filter.  Needs the default FIR variant. */
+ * pass.  freq_shift == 0: plain filter.  Needs the default FIR variant and
+ * the 1024-point block (ntaps <= 256); else VSIG_E_UNSUPPORTED (mix first). */
 int vsig_fir_exec_mix_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t n, void* y,
                           int64_t ny, double freq_shift, double sample_rate, int64_t i0);
 int vsig_fir_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* taps, int32_t ntaps,

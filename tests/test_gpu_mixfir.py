@@ -98,3 +98,14 @@ def test_stream_chain_with_frequency_shift(gpu, decim):
     _close(ch.y.cpu().numpy(), yr)
     m, lag, s1, s2, nout = ch.global_peak()
     assert lag == ref.xcorr_peak(yr, tmpl, "valid")[1] == k0 // decim
+
+
+def test_long_filter_with_frequency_shift(gpu):
+    """ntaps > 256 (4096-point blocks): the standalone mixer runs first, then
+    the filter -- the same result contract."""
+    n = 300_001
+    x = ref.synth_iq(n, seed=8)
+    taps = scipy.signal.firwin(400, 0.1).astype(np.float32)
+    y = gpu.filter(x, taps, 2, freq_shift=FS, sample_rate=SR)
+    r = ref.fir_filter(ref.apply_frequency_shift(x, FS, SR), taps, 2)
+    _close(y, r)

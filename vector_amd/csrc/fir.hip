@@ -246,7 +246,7 @@ hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0,
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
   const dim3 g((unsigned)((nblocks + 1) / 2)), blk(Plan1024s::TF);
-  const MixArgs m = mix ? *mix : MixArgs{0.0, 1.0, 0};
+  const MixArgs m = mix ? *mix : MixArgs{};
 #define VSIG_FD(PD)                                                                              \
   do {                                                                                           \
     if (mix)                                                                                     \
@@ -266,7 +266,7 @@ hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0,
 template <class PL, int PERSIST, bool MIX = false>
 void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, int ntaps,
                   long long hop, int decim, float2* y, long long nblocks, const float2* tw,
-                  hipStream_t st, MixArgs mix = MixArgs{0.0, 1.0, 0}) {
+                  hipStream_t st, MixArgs mix = MixArgs{}) {
   const long long grid =
       (PERSIST == 1 || PERSIST == 2)
           ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks)
@@ -280,11 +280,9 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
                          int variant, hipStream_t st, const MixArgs* mix) {
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
-  if (mix) {   // fused mixer: the default pair kernel (register anchors) only
-    if ((variant & (8 | 16 | 128)) || !(variant & 64)) return hipErrorInvalidValue;
-    VSIG_OS_SWITCH(M, variant, {
-      launch_fir_t<PL, 6, true>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st, *mix);
-    });
+  if (mix) {   // fused mixer: the default one-wave pair kernel (M = 1024) only
+    if ((variant & (8 | 16 | 128)) || !(variant & 64) || M != 1024) return hipErrorInvalidValue;
+    launch_fir_t<Plan1024s, 6, true>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st, *mix);
     return hipGetLastError();
   }
   VSIG_OS_SWITCH(M, variant, {

@@ -74,14 +74,21 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
 }
 
 // load_segment with the NCO mixer applied to each sample (global index
-// mix.i0 + s0 + i; the zero fill stays zero).
+// mix.i0 + s0 + i; the zero fill stays zero): one double-precision phase per
+// lane (sample g + t), then the per-element offsets' rotations
+// (offsets 64 e, mix.rot) in fp32 -- about 2e-7 relative per sample.
 template <class P>
 __device__ __forceinline__ void load_segment_mix(float2* v, const float2* __restrict__ x,
                                                  long long s0, long long n, int t, const MixArgs& mix) {
+  static_assert(P::TF == 64 && P::E == 16 && P::R[0] == 16,
+                "the rotation table assumes in_index(t, e) = t + 64 e");
   load_segment<P>(v, x, s0, n, t);
-  const long long g = mix.i0 + s0;
+  const float2 r0 = mix_rot_fast(mix.i0 + s0 + t, mix.wsr);
 #pragma unroll
-  for (int e = 0; e < P::E; ++e) v[e] = mix_at(v[e], g + in_index<P>(t, e), mix.w, mix.sr);
+  for (int e = 0; e < P::E; ++e) {
+    const float2 r = cmul(r0, make_float2(mix.rot[2 * e], mix.rot[2 * e + 1]));
+    v[e] = cmul(v[e], r);
+  }
 }
 
 // ---------------------------------------------------------------------------

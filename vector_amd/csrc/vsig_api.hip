@@ -533,8 +533,8 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
                                    tw, twd, c->stream, mix));
     return VSIG_OK;
   }
-  if (mix && ((c->var.fir & (8 | 16 | 128)) || !(c->var.fir & 64)))
-    return fail(c, VSIG_E_UNSUPPORTED, "fused mixer needs the default FIR variant");
+  if (mix && ((c->var.fir & (8 | 16 | 128)) || !(c->var.fir & 64) || f->M != 1024))
+    return fail(c, VSIG_E_UNSUPPORTED, "fused mixer needs the default FIR variant and ntaps <= 256");
   rc = get_tw_for(c, f->M, c->var.fir, true, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
@@ -577,7 +577,17 @@ int vsig_fir_exec_mix_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, 
   if (!f) return VSIG_E_INVALID;
   if (freq_shift == 0.0) return fir_exec(f, x, nhist, n, y, ny, nullptr);   // utils.py:122-123
   if (!(sample_rate != 0.0)) return fail(f->ctx, VSIG_E_INVALID, "sample_rate must be non-zero");
-  const vsig::MixArgs m{(2.0 * M_PI) * freq_shift, sample_rate, (long long)i0};
+  const double w = (2.0 * M_PI) * freq_shift;
+  vsig::MixArgs m{};
+  m.w = w;
+  m.sr = sample_rate;
+  m.i0 = (long long)i0;
+  m.wsr = w / sample_rate;
+  for (int e = 0; e < 16; ++e) {       // exp(j wsr 64 e), reduced mod 2 pi in double
+    const double a = std::remainder(m.wsr * 64.0 * e, 2.0 * M_PI);
+    m.rot[2 * e] = (float)std::cos(a);
+    m.rot[2 * e + 1] = (float)std::sin(a);
+  }
   return fir_exec(f, x, nhist, n, y, ny, &m);
 }
 

@@ -42,6 +42,13 @@ enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
 struct MixArgs {
   double w, sr;
   long long i0;      // global sample index of x[0]
+  double wsr;        // w / sr (the fused loads' phase slope)
+  // exp(j wsr d_e) for the fused loads' element offsets d_e = 64 e (the
+  // 1024-point one-wave plan, 16 elements per lane), formed in double on the
+  // host and rounded once to fp32: a lane rotates by exp(j theta(g + t)) once
+  // and then by these, so the double-precision phase runs once per segment
+  // and lane instead of once per sample.
+  float rot[32];     // (cos, sin) interleaved
 };
 __device__ __forceinline__ float2 mix_at(float2 v, long long gi, double w, double sr) {
   constexpr double kTwoPiHi = 6.28318530717958623200e+00;
@@ -54,6 +61,33 @@ __device__ __forceinline__ float2 mix_at(float2 v, long long gi, double w, doubl
   float s, c;
   sincosf((float)r, &s, &c);
   return make_float2(v.x * c - v.y * s, v.x * s + v.y * c);
+}
+
+// The fused loads' form: exp(j theta), theta = (w / sr) * gi, one double
+// multiply instead of numpy's division then multiply (|difference| <= ~2 ulp
+// of theta, e.g. 2e-7 rad at |theta| = 1e9 rad; the standalone mixer keeps
+// numpy's order).
+// exp(2 pi j rev) for a phase given in revolutions (double): reduced in double
+// to a quarter turn q and |g| <= 1/8 turn, then fp32 Taylor polynomials to
+// degree 9 / 10 on |2 pi g| <= pi/4 (truncation < 2e-9); no ocml sincosf, whose
+// large-argument path keeps a private array in scratch.
+__device__ __forceinline__ float2 cis_rev(double rev) {
+  const double f = rev - rint(rev);                    // [-1/2, 1/2] turn
+  const double q = rint(4.0 * f);                      // quarter turns, -2..2
+  const float x = (float)(f - 0.25 * q) * 6.283185307179586f;   // |x| <= pi/4
+  const float x2 = x * x;
+  const float sn = x * fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, 2.7557319e-6f, -1.9841270e-4f),
+                                              8.3333333e-3f), -1.6666667e-1f), 1.0f);
+  const float cs = fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, fmaf(x2, -2.7557319e-7f, 2.4801587e-5f),
+                                                    -1.3888889e-3f), 4.1666667e-2f), -0.5f), 1.0f);
+  const int qi = ((int)q) & 3;                         // rotate by q quarter turns
+  const float c = qi == 0 ? cs : qi == 1 ? -sn : qi == 2 ? -cs : sn;
+  const float s = qi == 0 ? sn : qi == 1 ? cs : qi == 2 ? -sn : -cs;
+  return make_float2(c, s);
+}
+__device__ __forceinline__ float2 mix_rot_fast(long long gi, double wsr) {
+  constexpr double kInvTwoPi = 1.59154943091895345608e-01;
+  return cis_rev((wsr * kInvTwoPi) * (double)gi);
 }
 
 // One block's |c| reduction partial (also the layout of the final result).

@@ -236,6 +236,14 @@ class FirFilter:
         if out is None:
             out = torch.empty(ny, dtype=torch.complex64, device=x.device)
         _check_dev(out, ny, torch.complex64, "filter output", self.ctx.device)
+        if freq_shift and self.block != 1024:
+            # long filters (M > 1024): the standalone mixer first, same phase origin
+            xm = torch.empty_like(x)
+            w = (2j * np.pi * freq_shift).imag
+            self.ctx.check(self.ctx.lib.vsig_mix_c64_dev(self.ctx.h, _ptr(x), int(x.shape[0]),
+                                                         float(w), float(sample_rate), int(i0),
+                                                         _ptr(xm)), "mix")
+            x, freq_shift = xm, 0.0
         if freq_shift:
             self.ctx.check(self.ctx.lib.vsig_fir_exec_mix_dev(
                 self.h, _ptr(x), int(nhist), n, _ptr(out), ny, float(freq_shift),
