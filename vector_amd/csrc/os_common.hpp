@@ -36,6 +36,9 @@ constexpr int min_waves() {
 #ifdef VSIG_EXP_SPLIT_W4
   return PERSIST == 4 ? 4 : 1;
 #else
+#ifdef VSIG_EXP_PAIR_W
+  if (PERSIST == 6 && P::TF == 64) return VSIG_EXP_PAIR_W;
+#endif
   return (PERSIST == 4 && P::E <= 16) ? 4 : 1;
 #endif
 }
