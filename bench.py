@@ -252,6 +252,9 @@ def main():
                 "algorithmic_bytes": bytes_per_launch[dom],
                 "avg_launch_ms": round(stages[dom], 4),
                 "traffic_source": pmc["source"] if pmc else None}
+        if pmc and "valu_issue_frac" in pmc:
+            # the correlator is VALU-bound: its issue utilisation from the same PMC pass
+            roof["valu_issue_frac"] = pmc["valu_issue_frac"]
     # every stage against its own roof: HBM bytes for all three, and for the
     # correlator (not HBM-bound) the FP32 vector roof with the standard
     # 5 N log2 N FFT flop count (2 FFTs + the spectrum multiply per block)
@@ -260,6 +263,10 @@ def main():
         gbs = bytes_per_launch[k] / (ms * 1e-3) / 1e9
         stage_roof[k] = {"ms": round(ms, 4), "bytes": bytes_per_launch[k], "GBs": round(gbs, 1),
                          "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+        pk = load_traffic(f"{k}:n={n}:ntaps={args.ntaps}:decim={args.decim}:nfft={args.nfft}:"
+                          f"L={args.template}")
+        if pk and "valu_issue_frac" in pk:
+            stage_roof[k]["valu_issue_frac"] = pk["valu_issue_frac"]
     if "xcorr" in stages:
         M = xcorr_block(args.template, args.xcorr_m)
         L = args.template
@@ -366,6 +373,8 @@ def run_sync(args, world, rank, local, dev):
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                 "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
                 "traffic_source": pmc["source"] if pmc else None}
+        if pmc and "valu_issue_frac" in pmc:
+            roof["valu_issue_frac"] = pmc["valu_issue_frac"]
         stage = {"xcorr": {"ms": round(ms, 4), "TFLOPs": round(tf, 2),
                            "valu_peak_TFLOPs": FP32_PEAK_TF, "valu_frac": round(tf / FP32_PEAK_TF, 4),
                            "M": M}}

@@ -58,6 +58,11 @@ def main(src, dst, keyspec):
             d["frac_wait_any"] = med.get("SQ_WAIT_ANY", 0) / wc
             d["frac_wait_inst"] = med.get("SQ_WAIT_INST_ANY", 0) / wc
             d["frac_active"] = med.get("SQ_ACTIVE_INST_ANY", 0) / wc
+        if "SQ_INSTS_VALU" in med and med.get("GRBM_GUI_ACTIVE"):
+            # VALU issue utilisation: wave64 VALU instructions x 4 issue cycles
+            # (MI355X_MICROARCH.md issue-cost table) over 256 CUs x 4 SIMDs x the
+            # launch's busy cycles (GRBM_GUI_ACTIVE is summed over the 8 XCDs)
+            d["valu_issue_frac"] = med["SQ_INSTS_VALU"] * 4 / (1024 * med["GRBM_GUI_ACTIVE"] / 8)
         out["kernels"][fam] = d
     json.dump(out, open(dst, "w"), indent=1)
     # per-kernel files bench.py looks up (config_key match)
@@ -65,6 +70,8 @@ def main(src, dst, keyspec):
         if "hbm_bytes_per_launch" in d:
             rec = {"config_key": f"{fam}:{keyspec}", "hbm_bytes_per_launch": d["hbm_bytes_per_launch"],
                    "source": f"{os.path.basename(dst)} (rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE)"}
+            if "valu_issue_frac" in d:
+                rec["valu_issue_frac"] = round(d["valu_issue_frac"], 4)
             out["kernels"][fam]["bench_record"] = rec
             tag = os.path.basename(dst)[len("pmc_"):] if os.path.basename(dst).startswith("pmc_") \
                 else os.path.basename(dst)
