@@ -69,3 +69,14 @@ def test_split_first_fir_matches_single_launch(gpu, decim):
     got = ch.y.cpu().numpy()
     w = want.cpu().numpy()
     assert np.abs(got - w).max() <= 1e-5 * np.abs(w).max()
+
+
+def test_c_example_runs(gpu, tmp_path):
+    """examples/chain_c.c: filter -> spectrogram -> sync through the C ABI from
+    a C program (child process); exit 0 = the preamble found at its offset."""
+    import subprocess
+    from test_host_cpu import _build_c_example
+    exe = _build_c_example(str(tmp_path / "chain_c"))
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "planted 300001" in r.stdout

@@ -140,3 +140,23 @@ def test_correlate_offsets_model():
         v = rng.standard_normal(nv) + 1j * rng.standard_normal(nv)
         for mode in ("full", "valid", "same"):
             np.testing.assert_allclose(model(a, v, mode), np.correlate(a, v, mode), atol=1e-12)
+
+
+def _build_c_example(out):
+    import shutil
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.path.join(root, "vector_amd", "libvsig.so")
+    if shutil.which("gcc") is None or not os.path.exists(lib):
+        pytest.skip("gcc or libvsig.so missing")
+    cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
+           os.path.join(root, "examples", "chain_c.c"), "-L", os.path.dirname(lib), "-lvsig",
+           f"-Wl,-rpath,{os.path.dirname(lib)}", "-lm", "-o", out]
+    subprocess.run(cmd, check=True)
+    return out
+
+
+def test_c_example_compiles(tmp_path):
+    """include/vsig.h is plain C99 and examples/chain_c.c links against the
+    library's exported symbols (the non-Python binding of INTEGRATION.md)."""
+    assert os.path.exists(_build_c_example(str(tmp_path / "chain_c")))
