@@ -141,6 +141,8 @@ def main():
     ap.add_argument("--freq-shift", type=float, default=0.0,
                     help="NCO mixer (apply_frequency_shift) fused into the FIR loads, Hz")
     ap.add_argument("--sample-rate", type=float, default=2e9, help="for --freq-shift (config 5: 2 GS/s)")
+    ap.add_argument("--three-streams", action="store_true",
+                    help="FIR / PSD / xcorr on their own HIP streams (default: one stream)")
     ap.add_argument("--fuse", action="store_true",
                     help="FIR and PSD in one fused launch (D=1, nfft 8192; default: two launches)")
     ap.add_argument("--workload", choices=("chain", "pfb", "sync"), default="chain",
@@ -180,6 +182,7 @@ def main():
             ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, k.encode(), v), k)
     cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl,
                       pipeline=args.pipeline, serial=args.serial, fuse=args.fuse,
+                      one_stream=not args.three_streams,
                       freq_shift=args.freq_shift, sample_rate=args.sample_rate)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)

@@ -49,6 +49,8 @@ class ChainConfig:
                                  # (a sub-chunk's filtered samples are re-read while cache-resident)
     freq_shift: float = 0.0      # apply_frequency_shift before the FIR (fused into its loads),
     sample_rate: float = 1.0     # phase from the global sample index (utils.py:120-127)
+    one_stream: bool = True      # pipeline == 1: all stages on the caller's stream (the PSD and
+                                 # correlator do not overlap anyway; saves the cross-stream waits)
     fuse: bool = False           # FIR + PSD in one launch where the backend has it (decim 1,
                                  # one sub-chunk): the PSD re-reads the filtered stream from cache
                                  # (measured slower than two launches on MI355X: DESIGN.md §4)
@@ -256,6 +258,8 @@ class StreamChain:
     def step(self):
         if self.cfg.serial:
             return self._step_serial()
+        if self.cfg.pipeline == 1 and self.cfg.one_stream:
+            return self._step_single()
         r, w, K = self.rank, self.world, self.cfg.pipeline
         be = self.be
         n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
@@ -298,6 +302,35 @@ class StreamChain:
                 self.peak_rows = rows
             else:
                 self.peak_rows = [self.recs]
+
+    def _step_single(self):
+        """One sub-chunk, every stage on the current stream: FIR (left halo
+        hidden behind its bulk), the right-halo exchange started behind it,
+        the PSD while the halo is in flight, then the correlator once it has
+        landed, then the peak records."""
+        r, w, n, ny, L = self.rank, self.world, self.cfg.n_local, self.ny, self.L
+        be = self.be
+        self._fir_first(be, n, ny)
+        reqs = []
+        if w > 1 and L > 1:
+            reqs = self._exchange_start(self.y_ext[: L - 1] if r > 0 else None,
+                                        r - 1 if r > 0 else None,
+                                        self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
+                                        r + 1 if r < w - 1 else None)
+        if not self.fused:
+            be.psd_into(self.y_ext[: ny], self.sxx)
+        if L:
+            self._exchange_wait(reqs)
+            halo = (L - 1) if r < w - 1 else 0
+            be.xcorr_peak(self.y_ext[: ny + halo], self.recs[0])
+            if w > 1:
+                rows = [torch.empty_like(self.recs) for _ in range(w)]
+                dist.all_gather(rows, self.recs, group=self.group)
+                self.peak_rows = rows
+            else:
+                self.peak_rows = [self.recs]
+        else:
+            self._exchange_wait(reqs)
 
     def _step_serial(self):
         """The same step with the sub-chunks run in order on the current stream,
