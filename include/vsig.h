@@ -163,8 +163,10 @@ int vsig_xcorr_exec_dev(vsig_xcorr* xc, const void* s, int64_t n, int32_t mode, 
                         vsig_peak_t* peak_dev);
 
 /* ---- general correlation, np.correlate(a, v, mode) semantics for any length
- * order (min(na, nv) <= 8192): output length full na+nv-1, valid
- * |na-nv|+1, same max(na, nv).  All pointers device (dev) or host. */
+ * order: output length full na+nv-1, valid |na-nv|+1, same max(na, nv).  The
+ * shorter operand up to 8192 samples runs as one streaming pass; longer ones
+ * as a sum over 8192-sample chunks of it (one pass per chunk, accumulated in
+ * c -- a device scratch c when c is NULL).  All pointers device (dev) or host. */
 int vsig_correlate_c64_dev(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,
                            int32_t mode, void* c, vsig_peak_t* peak_dev);
 int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,

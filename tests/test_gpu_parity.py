@@ -361,3 +361,35 @@ def test_decimating_fir_frequency_domain(gpu, decim, n):
         finally:
             ctx.lib.vsig_set_option(ctx.h, b"fir_variant", v.value)
             gpu.dsp._fir_cache.clear()
+
+
+@pytest.mark.parametrize("l1,l2", [(20_000, 61_234), (61_234, 20_000), (8193, 30_000),
+                                   (16_384, 16_384)])
+@pytest.mark.parametrize("mode", ["full", "valid", "same"])
+def test_cross_correlate_long_operands(gpu, l1, l2, mode):
+    """Both operands longer than 8192 (np.correlate has no limit): the shorter
+    one runs as a sum of 8192-sample chunks (one pass each, accumulated in c)."""
+    s1 = ref.synth_iq(l1, seed=l1)
+    s2 = ref.synth_iq(l2, seed=l2 + 1)
+    c, lags = gpu.cross_correlate_signals(s1, s2, mode)
+    cr, lr = ref.cross_correlate_signals(s1, s2, mode)
+    np.testing.assert_array_equal(lags, lr)
+    assert c.dtype == np.complex128 and c.shape == cr.shape
+    assert_normwise(c, cr, XC_TOL)
+
+
+def test_correlate_peak_long_template(gpu):
+    """A 20 000-sample QPSK reference planted in a 300 000-sample stream: exact
+    lag and peak through the chunked path, fused (no array) and via the array."""
+    L, n, k0 = 20_000, 300_000, 123_457
+    pre = ref.qpsk_preamble(L, seed=77)
+    s = ref.synth_iq(n, seed=78)
+    s[k0:k0 + L] += pre
+    want = ref.find_correlation_peak(*ref.cross_correlate_signals(pre, s, "valid"))
+    got = gpu.correlate_peak(pre, s, "valid")
+    assert got[0] == want[0] == k0
+    assert got[1] == pytest.approx(want[1], rel=1e-5)
+    assert got[2] == pytest.approx(want[2], rel=1e-4, abs=1e-6)
+    c, lags = gpu.cross_correlate_signals(pre, s, "valid")
+    got2 = gpu.find_correlation_peak(c, lags)
+    assert got2[0] == k0

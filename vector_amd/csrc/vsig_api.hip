@@ -673,6 +673,49 @@ int vsig_xcorr_exec_dev(vsig_xcorr* x, const void* s, int64_t n, int32_t mode, v
                    cout, peak_dev);
 }
 
+// Templates longer than 8192 (np.correlate has no length limit): the
+// template is cut into chunks of B = 8192 samples and the correlation is the
+// sum of the chunks' correlations, chunk p shifted by p B (kernel offset
+// off - p B, same output range); each chunk runs the M = 16384 correlator and
+// adds into c (store bit 8), then one peak reduction over the summed c
+// (first maximum, fp64 sums) gives find_correlation_peak's record.  Costs
+// ceil(L / 8192) passes over the stream plus the read-modify-write of c.
+static int correlate_chunked(vsig_ctx* c, const float2* tmpl, long long L, const float2* strm,
+                             long long n, long long off, long long nout, bool swap, float2* cout,
+                             vsig_peak_t* peak_dev) {
+  constexpr int B = 8192, M = 16384;
+  float2* cbuf = cout;
+  if (!cbuf) HIPCHK(c, hipMalloc(&cbuf, (size_t)nout * sizeof(float2)));
+  const float2 *tw, *wt;
+  int rc = 0;
+  const int var = (c->var.xcorr & 64) ? c->var.xcorr : 193;   // the half-frame kernel
+  if ((rc = (var & 8) ? get_tw2(c, 8192, &tw) : get_twiddles(c, 8192, &tw)) ||
+      (rc = get_half_tw(c, M, 256, &wt))) {
+    if (!cout) (void)hipFree(cbuf);
+    return rc;
+  }
+  for (long long p = 0; p * B < L && !rc; ++p) {
+    const int Lp = (int)((L - p * B) < B ? (L - p * B) : B);
+    float2* Ps = nullptr;
+    if ((rc = make_spectrum(c, tmpl + p * B, Lp, M, &Ps))) break;
+    const int mode = (swap ? 2 | 4 : 1) | (p ? 8 : 0);
+    {
+      Timed t(c, "xcorr");
+      hipError_t e = vsig::launch_xcorr_os(M, strm, n, Ps, off - p * B, nout, (long long)M - Lp + 1,
+                                           cbuf, mode, nullptr, tw, wt, var, c->stream);
+      if (e != hipSuccess) rc = fail(c, VSIG_E_HIP, hipGetErrorString(e));
+    }
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(Ps);
+  }
+  if (!rc) rc = vsig_peak_dev(c, VSIG_DTYPE_C64, cbuf, nout, peak_dev);   // null: c->result
+  if (!cout) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipFree(cbuf);
+  }
+  return rc;
+}
+
 int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
                            int32_t mode, void* cout, vsig_peak_t* peak_dev) {
   if (!c || !a || !v) return fail(c, VSIG_E_INVALID, "null pointer");
@@ -686,16 +729,18 @@ int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v
   const bool swap = nv > na;  // template must be the shorter operand
   const float2* tmpl = (const float2*)(swap ? a : v);
   const float2* strm = (const float2*)(swap ? v : a);
+  // c[o] = full[F + o]; full[i] = sum_k a[i-(nv-1)+k] conj(v[k]).
+  // Not swapped: kernel offset off = (L-1) - F.  Swapped: compute the
+  // correlation of v by a and store conj() reversed, off' = F + nout - nv.
+  const long long off = swap ? F + nout - nv : (nmin - 1) - F;
+  if (nmin > 8192) return correlate_chunked(c, tmpl, nmin, strm, nmax, off, nout, swap,
+                                            (float2*)cout, peak_dev);
   const int L = (int)nmin;
   const int M = os_size_xcorr(c, L);
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "shorter operand longer than 8192");
   float2* Ps = nullptr;
   int rc = make_spectrum(c, tmpl, L, M, &Ps);
   if (rc) return rc;
-  // c[o] = full[F + o]; full[i] = sum_k a[i-(nv-1)+k] conj(v[k]).
-  // Not swapped: kernel offset off = (L-1) - F.  Swapped: compute the
-  // correlation of v by a and store conj() reversed, off' = F + nout - nv.
-  const long long off = swap ? F + nout - nv : (L - 1) - F;
   rc = run_xcorr(c, M, Ps, nullptr, L, strm, nmax, off, nout,
                  (cout ? (swap ? 2 : 1) : 0) | (swap ? 4 : 0), cout,
                  peak_dev);

@@ -12,7 +12,11 @@ namespace vsig {
 // Epilogue: optional store of c (store_mode 1) or of conj(c) at nout-1-o
 // (store_mode 2, the swapped argument order of np.correlate), and the block's
 // |c| partial; store_mode bit 4 reports the argmax in the reversed index
-// space (first maximum of the reversed output).
+// space (first maximum of the reversed output); bit 8 adds to c instead of
+// storing (templates longer than 8192 run as a sum of template chunks).
+__device__ __forceinline__ void put_c(float2* p, float2 v, bool accum) {
+  *p = accum ? cadd(*p, v) : v;
+}
 // ---------------------------------------------------------------------------
 // Epilogue of one correlation block: |c|^2, block argmax / sums, optional store.
 template <class P>
@@ -24,19 +28,20 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
   const long long rem = nout - ob;
   const int lim = rem < hop ? (int)rem : (int)hop;
   const bool rev = store_mode & 4;
+  const bool accum = store_mode & 8;
   const int smode = store_mode & 3;
   // optional store: one uniform branch outside the element loops
   if (smode == 1) {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e);
-      if (i < lim) (c + ob)[(unsigned)i] = cconj(v[e]);
+      if (i < lim) put_c(c + ob + (unsigned)i, cconj(v[e]), accum);
     }
   } else if (smode == 2) {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e);
-      if (i < lim) (c + (nout - 1 - ob))[-i] = v[e];
+      if (i < lim) put_c(c + (nout - 1 - ob) - i, v[e], accum);
     }
   }
   if (!partials) return;
@@ -217,20 +222,21 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
   const long long rem = nout - ob;
   const int lim = rem < hop ? (int)rem : (int)hop;
   const bool rev = store_mode & 4;
+  const bool accum = store_mode & 8;
   const int smode = store_mode & 3;
   if (smode == 1) {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e);
-      if (i < lim) (c + ob)[(unsigned)i] = cconj(a[e]);
-      if (i + H < lim) (c + ob)[(unsigned)(i + H)] = cconj(d[e]);
+      if (i < lim) put_c(c + ob + (unsigned)i, cconj(a[e]), accum);
+      if (i + H < lim) put_c(c + ob + (unsigned)(i + H), cconj(d[e]), accum);
     }
   } else if (smode == 2) {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e);
-      if (i < lim) (c + (nout - 1 - ob))[-i] = a[e];
-      if (i + H < lim) (c + (nout - 1 - ob))[-(i + H)] = d[e];
+      if (i < lim) put_c(c + (nout - 1 - ob) - i, a[e], accum);
+      if (i + H < lim) put_c(c + (nout - 1 - ob) - (i + H), d[e], accum);
     }
   }
   if (!partials) return;
