@@ -96,6 +96,28 @@ def cpu_baseline(samples, taps, nfft, tmpl):
                 seconds=round(dt, 3))
 
 
+def cpu_baseline_allcores(samples, taps, nfft, tmpl, workers):
+    """The same CPU chain as cpu_baseline on `workers` processes, one time
+    chunk each with its halos (SURVEY.md §8(d)'s all-cores variant); value =
+    all chunks' samples / the wall time of the parallel map (worker start-up
+    and imports excluded by a warm-up map)."""
+    import multiprocessing as mp
+    from oracle import ref
+    ctx = mp.get_context("spawn")       # fresh interpreters: no GPU state in the workers
+    jobs = [(samples, 1000 + w, taps, nfft, tmpl) for w in range(workers)]
+    with ctx.Pool(workers) as pool:
+        pool.map(ref.chain_chunk_seconds, [(1 << 12, w, taps, nfft, tmpl) for w in range(workers)])
+        t0 = time.perf_counter()
+        secs = pool.map(ref.chain_chunk_seconds, jobs)
+        dt = time.perf_counter() - t0
+    return dict(value=round(workers * samples / dt / 1e6, 3), unit="Msamples/s", cores=workers,
+                kind="port",
+                sample=(f"{workers} processes x {samples} samples (2**{int(np.log2(samples))}) of "
+                        f"the chain with halos, {dt:.2f} s wall (per-chunk {min(secs):.2f}-"
+                        f"{max(secs):.2f} s)"),
+                seconds=round(dt, 3))
+
+
 def xcorr_block(L, forced):
     """Overlap-save block size the correlator plans for a template of L
     (vsig_api.hip os_size_xcorr, unless forced with --xcorr-m)."""
@@ -131,6 +153,8 @@ def main():
     ap.add_argument("--template", type=int, default=4096)
     ap.add_argument("--cpu-samples", type=int, default=1 << 22)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=16,
+                    help="processes for the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="sub-chunks per step: FIR / PSD / xcorr overlap on three HIP streams")
@@ -296,6 +320,12 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_samples, taps, args.nfft, tmpl)
         cpu["cores_available"] = len(os.sched_getaffinity(0))
+        if args.cpu_workers > 1:
+            try:
+                cpu["all_cores"] = cpu_baseline_allcores(args.cpu_samples // 2, taps, args.nfft,
+                                                         tmpl, args.cpu_workers)
+            except Exception as e:       # the GPU number stands without it
+                cpu["all_cores"] = {"error": repr(e)[:200]}
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "Msamples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),

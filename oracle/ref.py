@@ -377,3 +377,22 @@ def qpsk_preamble(L=4096, seed=4096):
     rng = np.random.default_rng(seed)
     b = rng.integers(0, 2, size=(2, L))
     return (((2 * b[0] - 1) + 1j * (2 * b[1] - 1)) / np.sqrt(2)).astype(np.complex64)
+
+
+def chain_chunk_seconds(args):
+    """The bench's CPU baseline for one time chunk (a pool worker: bench.py's
+    all-cores cpu_baseline leg maps it over chunks): FIR with
+    the chunk's (ntaps-1)-sample left halo, the spectrogram of the filtered
+    chunk, the valid correlation over it plus the next chunk's L-1 samples
+    (synthesised here: the timing, not the values, is the point) and
+    find_correlation_peak.  Returns the seconds the chunk took."""
+    import time
+    samples, seed, taps, nfft, tmpl = args
+    h, L = len(taps) - 1, len(tmpl)
+    x = synth_iq(h + samples + L - 1, seed=seed)
+    t0 = time.perf_counter()
+    y = np.convolve(x, taps)[h: h + samples + L - 1]
+    spectrum(y[:samples], 1.0, "hann", nfft, 0, nfft)
+    c, lags = cross_correlate_signals(tmpl, y, "valid")
+    find_correlation_peak(c, lags)
+    return time.perf_counter() - t0
