@@ -80,3 +80,28 @@ def test_c_example_runs(gpu, tmp_path):
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "planted 300001" in r.stdout
+
+
+def test_stream_chain_long_template(gpu):
+    """A 10 000-sample sync template (longer than one correlator chunk): the
+    chain's Correlator takes the chunked path; exact lag."""
+    import torch
+    from vector_amd.shard import ChainConfig, HipBackend, StreamChain
+    n, nfft, L = 1 << 20, 1024, 10_000
+    taps = scipy.signal.firwin(63, 0.3).astype(np.float32)
+    pre = ref.qpsk_preamble(L, seed=31)
+    tmpl = np.convolve(pre, taps)[:L].astype(np.complex64)
+    x = ref.synth_iq(n, seed=32)
+    k0 = 400_003
+    x[k0:k0 + L] += pre
+    cfg = ChainConfig(n_local=n, taps=taps, decim=1, nfft=nfft, template=tmpl)
+    ch = StreamChain(cfg, HipBackend(cfg, 0), 0, 1)
+    ch.x.copy_(torch.from_numpy(x))
+    ch.step()
+    torch.cuda.synchronize()
+    yr = ref.fir_filter(x, taps)
+    m, lag, s1, s2, nout = ch.global_peak()
+    i, rlag, peak, r1, r2, _ = ref.xcorr_peak(yr, tmpl, "valid")
+    assert lag == rlag == k0
+    assert m == pytest.approx(peak, rel=1e-4)
+    assert s1 == pytest.approx(r1, rel=1e-4)

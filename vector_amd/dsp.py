@@ -460,6 +460,13 @@ class Correlator:
             raise ValueError("v cannot be empty")
         self.ctx = _lib.get_context(device)
         self.L = int(t.size)
+        self.h = None
+        self.tmpl = None
+        if self.L > 8192:
+            # longer templates: the general correlation's chunked path (one
+            # pass per 8192-sample template chunk, accumulated; host-synchronous)
+            self.tmpl = torch.from_numpy(t).to(f"cuda:{self.ctx.device}")
+            return
         h = C.c_void_p()
         self.ctx.check(self.ctx.lib.vsig_xcorr_create(self.ctx.h, t.ctypes.data_as(C.c_void_p),
                                                       self.L, C.byref(h)), "vsig_xcorr_create")
@@ -481,6 +488,11 @@ class Correlator:
         if peak is None:
             peak = _peak_buffer(self.ctx)
         _check_dev(peak, 4, torch.float64, "peak record", self.ctx.device)
+        if self.tmpl is not None:
+            self.ctx.check(self.ctx.lib.vsig_correlate_c64_dev(
+                self.ctx.h, _ptr(s), ns, _ptr(self.tmpl), self.L, _lib.MODES[mode],
+                _ptr(out) if out is not None else None, _ptr(peak)), "xcorr (long template)")
+            return out, peak
         self.ctx.check(self.ctx.lib.vsig_xcorr_exec_dev(
             self.h, _ptr(s), int(s.shape[0]), _lib.MODES[mode],
             _ptr(out) if out is not None else None, _ptr(peak)), "xcorr")
