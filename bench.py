@@ -1,21 +1,22 @@
-"""Benchmark: Msamples/s of complex64 IQ through the FIR -> (decimate) -> FFT-PSD
+"""Benchmark: Msamples/s of complex64 IQ through the FIR -> decimate -> FFT-PSD
 -> xcorr-sync chain on 1..N MI355X GPUs, with the dominant kernel's achieved
 HBM bandwidth against the roofline and the CPU reference path beside it.
 
-Workload (BASELINE.json configs[1], extended with the sync stage the metric
-names): every rank owns a contiguous 2**28-sample (256 Msample, 2 GiB) time
-chunk of one long synthetic capture; 255-tap overlap-save FIR, D = 1;
-8192-point Hann PSD, hop 8192; 4096-sample template valid correlation with a
-fused |c| argmax.  Weak scaling: N GPUs process an N x 256 Msample capture
-(N = 8 is BASELINE config 5's 2**31 samples), exchanging only the FIR /
-correlation halos and 32-byte peak records over RCCL.
+Default workload = BASELINE configs[4] (config 5, the metric's full chain):
+one synthetic capture of 2**31 complex64 samples (2 GS/s for 1.07 s), 255-tap
+FIR, decimate by 4, 8192-point Hann PSD (hop 8192) of the decimated stream,
+4096-sample template valid correlation of the decimated stream with the fused
+|c| argmax (+ its exact refine).  Time-chunk partition: N GPUs own 2**31 / N
+contiguous samples each (strong scaling), exchanging only the FIR / correlation
+halos and 32-byte peak records over RCCL.
 
   python bench.py [--gpus N --steps K --warmup W]
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
-  python bench.py --workload pfb      # BASELINE config 4 (64-channel PFB), not the headline
-  python bench.py --workload sync     # BASELINE config 3 (4096-sample preamble over 2**30)
+  python bench.py --workload c2       # configs[1]: 2**28 samples / GPU, D = 1 (+ the sync
+                                      #   stage), north_star's FIR+FFT >= 70 % HBM target
+  python bench.py --workload sync     # configs[2]: 4096-sample preamble over 2**30
+  python bench.py --workload pfb      # configs[3]: 64-channel PFB, 2**29 samples / GPU
   python bench.py --freq-shift 3e8    # the chain with the NCO mixer fused into the FIR
-
 
 Inputs are generated on the device before timing (data resident in HBM).
 """
@@ -77,26 +78,26 @@ def generate_chunk(x: torch.Tensor, g0: int, seed: int, pre: np.ndarray, k0: int
         x[lo - g0:hi - g0] += torch.from_numpy(pre[lo - k0:hi - k0]).to(x.device)
 
 
-def cpu_baseline(samples, taps, nfft, tmpl):
+def cpu_baseline(samples, taps, nfft, tmpl, decim=1):
     """The reference's CPU path (oracle: np.convolve / scipy.signal.spectrogram /
     np.correlate, single-threaded numpy) timed on a bounded sample."""
     from oracle import ref
     x = ref.synth_iq(samples, seed=99)
     t0 = time.perf_counter()
-    y = ref.fir_filter(x, taps, 1)
+    y = ref.fir_filter(x, taps, decim)
     ref.spectrum(y, 1.0, "hann", nfft, 0, nfft)
     c, lags = ref.cross_correlate_signals(tmpl, y, "valid")
     ref.find_correlation_peak(c, lags)
     dt = time.perf_counter() - t0
     return dict(value=round(samples / dt / 1e6, 3), unit="Msamples/s", cores=1, kind="port",
                 sample=(f"{samples} samples (2**{int(np.log2(samples))}) of the same chain: "
-                        f"np.convolve {len(taps)} taps, scipy spectrogram nfft={nfft}, "
+                        f"np.convolve {len(taps)} taps + [::{decim}], scipy spectrogram nfft={nfft}, "
                         f"np.correlate complex128 L={len(tmpl)} valid + find_correlation_peak; "
                         f"{dt:.2f} s, 1 thread"),
                 seconds=round(dt, 3))
 
 
-def cpu_baseline_allcores(samples, taps, nfft, tmpl, workers):
+def cpu_baseline_allcores(samples, taps, nfft, tmpl, workers, decim=1):
     """The same CPU chain as cpu_baseline on `workers` processes, one time
     chunk each with its halos (SURVEY.md §8(d)'s all-cores variant); value =
     all chunks' samples / the wall time of the parallel map (worker start-up
@@ -104,9 +105,10 @@ def cpu_baseline_allcores(samples, taps, nfft, tmpl, workers):
     import multiprocessing as mp
     from oracle import ref
     ctx = mp.get_context("spawn")       # fresh interpreters: no GPU state in the workers
-    jobs = [(samples, 1000 + w, taps, nfft, tmpl) for w in range(workers)]
+    jobs = [(samples, 1000 + w, taps, nfft, tmpl, decim) for w in range(workers)]
     with ctx.Pool(workers) as pool:
-        pool.map(ref.chain_chunk_seconds, [(1 << 12, w, taps, nfft, tmpl) for w in range(workers)])
+        pool.map(ref.chain_chunk_seconds, [(1 << 15, w, taps, nfft, tmpl, decim)
+                                           for w in range(workers)])
         t0 = time.perf_counter()
         secs = pool.map(ref.chain_chunk_seconds, jobs)
         dt = time.perf_counter() - t0
@@ -118,11 +120,9 @@ def cpu_baseline_allcores(samples, taps, nfft, tmpl, workers):
                 seconds=round(dt, 3))
 
 
-def xcorr_block(L, forced):
+def xcorr_block(L):
     """Overlap-save block size the correlator plans for a template of L
-    (vsig_api.hip os_size_xcorr, unless forced with --xcorr-m)."""
-    if forced:
-        return forced
+    (vsig_api.hip os_size_xcorr)."""
     return 4096 if L <= 1024 else 8192 if L <= 2048 else 16384
 
 
@@ -141,14 +141,26 @@ def load_traffic(key):
     return best
 
 
+WORKLOADS = {
+    # name: (decim, samples, per_gpu (weak) or total (strong), label)
+    "c5": (4, 1 << 31, False, "BASELINE configs[4]: full chain FIR -> decimate 4 -> FFT PSD -> "
+                              "xcorr over a 2**31-sample capture, time-chunk partition"),
+    "c2": (1, 1 << 28, True, "BASELINE configs[1] chain + sync: 2**28 samples per GPU, D = 1"),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--samples", type=int, default=1 << 28, help="input samples per GPU")
+    ap.add_argument("--workload", choices=("c5", "c2", "pfb", "sync"), default="c5",
+                    help="c5: the metric's full chain (default); c2: 2**28/GPU, D=1; "
+                         "sync: config 3 preamble correlation over 2**30 samples; pfb: config 4")
+    ap.add_argument("--samples", type=int, default=None,
+                    help="input samples per GPU (default: the workload's)")
     ap.add_argument("--ntaps", type=int, default=255)
-    ap.add_argument("--decim", type=int, default=1)
+    ap.add_argument("--decim", type=int, default=None, help="(default: the workload's)")
     ap.add_argument("--nfft", type=int, default=8192)
     ap.add_argument("--template", type=int, default=4096)
     ap.add_argument("--cpu-samples", type=int, default=1 << 22)
@@ -156,26 +168,19 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="processes for the all-cores CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-refine", action="store_true",
+                    help="skip the correlator's exact-argmax refine pass (A/B only)")
     ap.add_argument("--pipeline", type=int, default=1,
                     help="sub-chunks per step: FIR / PSD / xcorr overlap on three HIP streams")
     ap.add_argument("--serial", action="store_true",
                     help="run the --pipeline sub-chunks in order on one stream (cache reuse)")
-    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m", "fir_psd_variant", "psd_grid"):
-        ap.add_argument("--" + k.replace("_", "-"), type=int, default=None)
     ap.add_argument("--freq-shift", type=float, default=0.0,
                     help="NCO mixer (apply_frequency_shift) fused into the FIR loads, Hz")
     ap.add_argument("--sample-rate", type=float, default=2e9, help="for --freq-shift (config 5: 2 GS/s)")
     ap.add_argument("--three-streams", action="store_true",
                     help="FIR / PSD / xcorr on their own HIP streams (default: one stream)")
-    ap.add_argument("--fuse", action="store_true",
-                    help="FIR and PSD in one fused launch (D=1, nfft 8192; default: two launches)")
-    ap.add_argument("--workload", choices=("chain", "pfb", "sync"), default="chain",
-                    help="chain: the headline FIR->PSD->xcorr metric; pfb: config 4 channelizer; "
-                         "sync: config 3 preamble correlation over 2**30 samples")
     ap.add_argument("--nchan", type=int, default=64)
     ap.add_argument("--branch-taps", type=int, default=16)
-    ap.add_argument("--pfb-variant", type=int, default=None)
-    ap.add_argument("--pfb-fpg", type=int, default=None)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -196,23 +201,29 @@ def main():
         return run_sync(args, world, rank, local, dev)
     from vector_amd.shard import ChainConfig, HipBackend, StreamChain
 
-    n = args.samples
-    taps, pre, tmpl = design(args.ntaps, args.template, args.decim)
+    wdecim, wsamples, weak, wlabel = WORKLOADS[args.workload]
+    decim = args.decim if args.decim is not None else wdecim
+    if args.samples is not None:
+        n = args.samples
+    else:
+        n = wsamples if weak else wsamples // world
+    granule = args.nfft * decim
+    if n % granule:
+        raise SystemExit(f"samples per GPU ({n}) must be a multiple of nfft * decim ({granule})")
+    taps, pre, tmpl = design(args.ntaps, args.template, decim)
     from vector_amd._lib import get_context
     ctx0 = get_context(local)
-    for k in ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m", "fir_psd_variant", "psd_grid"):
-        v = getattr(args, k)
-        if v is not None:
-            ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, k.encode(), v), k)
-    cfg = ChainConfig(n_local=n, taps=taps, decim=args.decim, nfft=args.nfft, template=tmpl,
-                      pipeline=args.pipeline, serial=args.serial, fuse=args.fuse,
+    if args.no_refine:
+        ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, b"refine", 0), "refine")
+    cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=args.nfft, template=tmpl,
+                      pipeline=args.pipeline, serial=args.serial,
                       one_stream=not args.three_streams,
                       freq_shift=args.freq_shift, sample_rate=args.sample_rate)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)
     N = world * n
-    ny_total = N // args.decim
-    k0 = (ny_total // 2 + 12_345) * args.decim     # global input sample of the preamble
+    ny_total = N // decim
+    k0 = (ny_total // 2 + 12_345) * decim     # global input sample of the preamble
     if args.freq_shift:   # plant the preamble so that it leaves the mixer unrotated
         ph = 2 * np.pi * args.freq_shift * ((k0 + np.arange(len(pre))) / args.sample_rate)
         pre = (pre * np.exp(-1j * ph)).astype(np.complex64)
@@ -248,18 +259,16 @@ def main():
     # per-kernel durations from HIP events on the launch stream
     import ctypes as C
     stages = {}
-    for name in ("fir", "psd", "fir_psd", "xcorr"):
+    for name in ("fir", "psd", "xcorr", "refine"):
         tot, cnt = C.c_double(), C.c_int64()
         lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
         if cnt.value:
             stages[name] = tot.value / cnt.value
-    ny = n // args.decim
-    # fir_psd (fused): x read + y written + Sxx written; the PSD's re-read of y
-    # is served by L2 / the Infinity Cache (PMC traffic in profiles/ checks it)
+    ny = n // decim
     bytes_per_launch = {"fir": 8 * n + 8 * ny, "psd": 8 * ny + 4 * ny,
-                        "fir_psd": 8 * n + 8 * ny + 4 * ny, "xcorr": 8 * (ny + chain.yhalo)}
+                        "xcorr": 8 * (ny + chain.yhalo)}
     m, lag, s1, s2, nout = chain.global_peak()
-    check = {"sync_lag": lag, "expected": k0 // args.decim, "ok": bool(lag == k0 // args.decim)}
+    check = {"sync_lag": lag, "expected": k0 // decim, "ok": bool(lag == k0 // decim)}
 
     if rank != 0:
         if world > 1:
@@ -268,34 +277,36 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     value = N / (elapsed / args.steps) / 1e6
     roof = None
-    if stages:
-        dom = max(stages, key=lambda k: stages[k])
-        achieved = bytes_per_launch[dom] / (stages[dom] * 1e-3) / 1e9
-        key = f"{dom}:n={n}:ntaps={args.ntaps}:decim={args.decim}:nfft={args.nfft}:L={args.template}"
+    kstages = {k: v for k, v in stages.items() if k in bytes_per_launch}
+    if kstages:
+        dom = max(kstages, key=lambda k: kstages[k])
+        achieved = bytes_per_launch[dom] / (kstages[dom] * 1e-3) / 1e9
+        key = f"{dom}:n={n}:ntaps={args.ntaps}:decim={decim}:nfft={args.nfft}:L={args.template}"
         pmc = load_traffic(key)
         roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                 "algorithmic_bytes": bytes_per_launch[dom],
-                "avg_launch_ms": round(stages[dom], 4),
+                "avg_launch_ms": round(kstages[dom], 4),
                 "traffic_source": pmc["source"] if pmc else None}
         if pmc and "valu_issue_frac" in pmc:
-            # the correlator is VALU-bound: its issue utilisation from the same PMC pass
             roof["valu_issue_frac"] = pmc["valu_issue_frac"]
     # every stage against its own roof: HBM bytes for all three, and for the
     # correlator (not HBM-bound) the FP32 vector roof with the standard
     # 5 N log2 N FFT flop count (2 FFTs + the spectrum multiply per block)
     stage_roof = {}
-    for k, ms in stages.items():
+    for k, ms in kstages.items():
         gbs = bytes_per_launch[k] / (ms * 1e-3) / 1e9
         stage_roof[k] = {"ms": round(ms, 4), "bytes": bytes_per_launch[k], "GBs": round(gbs, 1),
                          "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
-        pk = load_traffic(f"{k}:n={n}:ntaps={args.ntaps}:decim={args.decim}:nfft={args.nfft}:"
+        pk = load_traffic(f"{k}:n={n}:ntaps={args.ntaps}:decim={decim}:nfft={args.nfft}:"
                           f"L={args.template}")
-        if pk and "valu_issue_frac" in pk:
-            stage_roof[k]["valu_issue_frac"] = pk["valu_issue_frac"]
+        if pk:
+            stage_roof[k]["traffic"] = pk["hbm_bytes_per_launch"]
+            if "valu_issue_frac" in pk:
+                stage_roof[k]["valu_issue_frac"] = pk["valu_issue_frac"]
     if "xcorr" in stages:
-        M = xcorr_block(args.template, args.xcorr_m)
+        M = xcorr_block(args.template)
         L = args.template
         hop = M - L + 1
         nb = -(-(ny + chain.yhalo - L + 1) // hop)
@@ -304,42 +315,50 @@ def main():
         stage_roof["xcorr"].update({"flops": int(flops), "TFLOPs": round(tf, 2),
                                     "valu_peak_TFLOPs": FP32_PEAK_TF,
                                     "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
-    # north_star's FIR+FFT target on SURVEY.md §8(d) C2's unfused byte count
-    # (28 B/sample: filter() writes y, spectrum() reads it); with the fused
-    # kernel the HBM bytes actually moved are 20 B/sample (stage "fir_psd")
-    fp_ms = (stages["fir"] + stages["psd"]) if ("fir" in stages and "psd" in stages) \
-        else stages.get("fir_psd")
-    if fp_ms:
+    if "refine" in stages:
+        stage_roof["refine"] = {"ms": round(stages["refine"], 4)}
+    # north_star's FIR+FFT target on SURVEY.md §8(d)'s unfused byte count
+    # (filter() writes y, spectrum() reads it): 8 + 8/D + 12/D B/sample
+    if "fir" in stages and "psd" in stages:
+        fp_ms = stages["fir"] + stages["psd"]
         b = bytes_per_launch["fir"] + bytes_per_launch["psd"]
         t = fp_ms * 1e-3
         stage_roof["fir+psd"] = {"ms": round(fp_ms, 4), "GBs": round(b / t / 1e9, 1),
                                  "hbm_frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
-                                 "bytes_basis": "28 B/sample (unfused FIR 16 + PSD 12)",
-                                 "fused": "fir_psd" in stages}
+                                 "bytes_basis": f"{b / n:.0f} B/sample (FIR 8 + 8/D, PSD 12/D)"}
+    # the whole step against the chain's algorithmic bytes (SURVEY.md §8(d):
+    # 28 B/sample at D = 1 plus the correlator's 8, 15 B/sample at D = 4)
+    chain_bytes = sum(bytes_per_launch.values())
+    stage_roof["chain"] = {"ms": round(ms_per_step, 4), "bytes_per_gpu": chain_bytes,
+                           "GBs_per_gpu": round(chain_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                           "hbm_frac": round(chain_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "bytes_basis": f"{chain_bytes / n:.2f} B/input sample"}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_samples, taps, args.nfft, tmpl)
+        cs = args.cpu_samples
+        cpu = cpu_baseline(cs, taps, args.nfft, tmpl, decim)
         cpu["cores_available"] = len(os.sched_getaffinity(0))
         if args.cpu_workers > 1:
             try:
-                cpu["all_cores"] = cpu_baseline_allcores(args.cpu_samples // 2, taps, args.nfft,
-                                                         tmpl, args.cpu_workers)
+                cpu["all_cores"] = cpu_baseline_allcores(cs // 2, taps, args.nfft, tmpl,
+                                                         args.cpu_workers, decim)
             except Exception as e:       # the GPU number stands without it
                 cpu["all_cores"] = {"error": repr(e)[:200]}
     out = {
         "metric": METRIC, "value": round(value, 1), "unit": "Msamples/s", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "c64 (fp32)",
+        "higher_is_better": True, "scaling": "weak" if (weak or args.samples is not None) else "strong",
+        "vs_baseline": None, "dtype": "c64 (fp32)",
         "data": "synthetic IQ generated on device: 3 tones + CN(0,1) noise + QPSK preamble",
-        "config": {"workload": (f"BASELINE configs[1] chain + sync: {n} c64 samples/GPU, "
-                                f"{args.ntaps}-tap overlap-save FIR, D={args.decim}, "
-                                f"{args.nfft}-pt Hann PSD hop {args.nfft}, "
+        "config": {"workload": (f"{wlabel}: {n} c64 samples/GPU, {args.ntaps}-tap overlap-save "
+                                f"FIR, D={decim}, {args.nfft}-pt Hann PSD hop {args.nfft}, "
                                 f"{args.template}-sample template xcorr (valid) + argmax"),
-                   "samples_per_gpu": n, "total_samples": N, "ntaps": args.ntaps,
-                   "decim": args.decim, "nfft": args.nfft, "template": args.template,
+                   "name": args.workload, "samples_per_gpu": n, "total_samples": N,
+                   "ntaps": args.ntaps, "decim": decim, "nfft": args.nfft,
+                   "template": args.template,
                    "parallelism": f"time-chunk x{world} (RCCL halos)",
-                   "pipeline": args.pipeline, "serial": args.serial, "fused": chain.fused,
-                   "freq_shift": args.freq_shift},
+                   "pipeline": args.pipeline, "serial": args.serial,
+                   "freq_shift": args.freq_shift, "refine": not args.no_refine},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
@@ -362,10 +381,9 @@ def run_sync(args, world, rank, local, dev):
     from vector_amd import dsp
     if world != 1:
         raise SystemExit("--workload sync is BASELINE config 3 (one GPU)")
-    n = args.samples if args.samples != 1 << 28 else 1 << 30
+    n = args.samples if args.samples is not None else 1 << 30
     L = args.template
-    from oracle import ref            # preamble generator (same seed as the oracle's goldens)
-    pre = ref.qpsk_preamble(L, seed=4096)
+    _, pre, _ = design(args.ntaps, L)   # QPSK preamble, default_rng(4096)
     k0 = 123_456_789 if n > 123_456_789 + L else n // 3
     x = torch.empty(n, dtype=torch.complex64, device=dev)
     generate_chunk(x, 0, 20250718, pre, k0)
@@ -396,7 +414,7 @@ def run_sync(args, world, rank, local, dev):
         ms = tot.value / cnt.value
         nbytes = 8 * n
         ach = nbytes / (ms * 1e-3) / 1e9
-        M = xcorr_block(L, args.xcorr_m)
+        M = xcorr_block(L)
         nb = -(-nout // (M - L + 1))
         flops = nb * (2 * 5 * M * np.log2(M) + 6 * M)
         tf = flops / (ms * 1e-3) / 1e12
@@ -413,6 +431,7 @@ def run_sync(args, world, rank, local, dev):
                            "M": M}}
     cpu = None
     if not args.no_cpu_baseline:
+        from oracle import ref        # the CPU baseline leg only
         ns = 1 << 21
         xs = ref.synth_iq(ns, seed=99)
         t1 = time.perf_counter()
@@ -449,14 +468,10 @@ def run_pfb(args, world, rank, local, dev):
     import ctypes as C
     import scipy.signal
     from vector_amd.shard import HipPfbBackend, PfbChain
-    n = args.samples if args.samples != 1 << 28 else 1 << 29
+    n = args.samples if args.samples is not None else 1 << 29
     nchan, P = args.nchan, args.branch_taps
     proto = scipy.signal.firwin(P * nchan, 1.0 / nchan).astype(np.float32)
     be = HipPfbBackend(proto, nchan, local)
-    for k in ("pfb_variant", "pfb_fpg"):
-        v = getattr(args, k)
-        if v is not None:
-            be.ctx.check(be.ctx.lib.vsig_set_option(be.ctx.h, k.encode(), v), k)
     ch = PfbChain(n, proto, nchan, be, rank, world)
     generate_chunk(ch.x, rank * n, 20250718 + rank, np.zeros(0, np.complex64), -1)
     torch.cuda.synchronize()
@@ -488,10 +503,11 @@ def run_pfb(args, world, rank, local, dev):
         elapsed = float(t.item())
     tot, cnt = C.c_double(), C.c_int64()
     lib.vsig_timing_read(h, b"pfb", C.byref(tot), C.byref(cnt))
-    # spot check: the rank's frame 1 against the definition (oracle is test infra)
-    from oracle import ref
-    xs = ch.x_ext[: nchan + P * nchan].cpu().numpy()
-    want = ref.pfb_channelize(xs, proto, nchan)[:, 1]
+    # spot check: the rank's frame 1 against the PFB's definition (pfb.hip header),
+    # evaluated here in complex128 numpy
+    xs = ch.x_ext[nchan: nchan + P * nchan].cpu().numpy().astype(np.complex128)
+    z = (proto.astype(np.float64) * xs).reshape(P, nchan).sum(axis=0)
+    want = np.fft.fft(z)
     got = ch.frames()[1].cpu().numpy()
     err = float(np.abs(got - want).max() / np.abs(want).max())
     if rank != 0:

@@ -79,27 +79,28 @@ const char* vsig_last_error(const vsig_ctx* ctx);
  * stream.  A new context starts on a private non-blocking stream. */
 int vsig_set_stream(vsig_ctx* ctx, void* hip_stream);
 int vsig_synchronize(vsig_ctx* ctx);
-/* Tuning knobs (defaults are the measured best on MI355X):
- *   "psd_variant" / "fir_variant" / "xcorr_variant": bit 0 persistent kernel
- *   (next-unit prefetch, register twiddles), bit 1 (M = 16384) 512-thread plan,
- *   bit 3 LDS twiddles, bit 4 split re/im exchange, bit 5 (xcorr) partitioned
- *   template, bit 6 (xcorr, M = 16384) half-frame kernel (two blocks per CU);
- *   "fir_m" / "xcorr_m": overlap-save block size 4096 / 8192 / 16384, 0 = rule;
- *   "fir_psd_variant" (fused kernel): bit 0 non-temporal filtered-stream stores,
- *   bit 1 block barriers in the FIR phase, bit 2 next-round segment prefetch;
- *   "psd_grid": grid cap of the persistent PSD variants (0 = every resident slot).
- * Plans created afterwards use the new block sizes. */
+/* Options of the correlators' exact-argmax refine pass (refine.hip):
+ *   "refine"          1 (default): after every correlation, the outputs whose
+ *                     fp32 |c| lies within the band below the fp32 maximum are
+ *                     recomputed by direct sums in double precision (a
+ *                     compensated dot product for the final near-ties), in the
+ *                     operands' own precision, and the record's peak / index
+ *                     replaced -- np.argmax over numpy's complex128 sums;
+ *                     0: the fp32 FFT result only;
+ *   "refine_eps_ppm"  the band, relative to max |c| (default 1000 = 1e-3; the
+ *                     fp32 correlation error is ~1e-8 of |p| |s_segment|);
+ *   "refine_cap"      most outputs revisited (default 2^20); beyond it the
+ *                     record is left as the fp32 pass produced it and
+ *                     vsig_refine_status reports status 1. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
-/* Current value of a tuning knob (same keys as vsig_set_option). */
 int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
-/* Tuning micro-benchmark: `iters` in-LDS FFTs on each of `frames` frames of
- * the plan `key` (4096 / 8192 / 16384, -1024 / -2048 / -16384 for the
- * overlap-save one-wave and 512-thread plans); io: frames * |key| complex64. */
-/* HBM ceiling probe for the tuning tools: copy n complex64 x -> y with
- * variant 0: 8-B lanes, 1: 8-B + non-temporal stores, 2: 16-B lanes,
- * 3: 16-B + non-temporal stores; grid 0 = default. */
-int vsig_copy_bench(vsig_ctx* ctx, const void* x, int64_t n, void* y, int variant, int grid);
-int vsig_fft_bench(vsig_ctx* ctx, int key, void* io, int frames, int iters, int twl);
+/* Outcome of the context's last refine pass (synchronises the stream):
+ * status 0 refined, 1 skipped (more candidates than refine_cap), 2 no pass
+ * ran (refine off, or no correlation yet); candidates = candidate items. */
+int vsig_refine_status(vsig_ctx* ctx, int32_t* status, int64_t* candidates);
+/* Hash of the kernel / ABI sources this library was built from (the Python
+ * loader compares it with the sources next to it and refuses a stale build). */
+const char* vsig_build_id(void);
 /* Per-kernel timing with HIP events on the context stream (for bench.py):
  * enable, run, then read the mean duration in ms of each kernel family. */
 int vsig_timing_enable(vsig_ctx* ctx, int on);
@@ -143,30 +144,31 @@ int vsig_fir_exec_mix_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t n
                           int64_t ny, double freq_shift, double sample_rate, int64_t i0);
 int vsig_fir_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* taps, int32_t ntaps,
                  int32_t decim, void* y, int64_t ny);
-/* Fused filter -> spectrum of the filtered stream (one launch; the chain's
- * FIR + PSD stages, utils.py:281-291 applied to np.convolve's output):
- * y as vsig_fir_exec_hist_dev (decim must be 1), and sxx/nframes as
- * vsig_psd_c64_dev(y, ny, stride 1, win, nperseg = hop = nfft) with
- * nframes = ny / nfft.  Supported: nfft = 8192, the 1024-point FIR block
- * (ntaps <= 342); otherwise VSIG_E_UNSUPPORTED (run the two calls). */
-int vsig_fir_psd_exec_dev(vsig_fir* fir, const void* x, int64_t nhist, int64_t n, void* y,
-                          int64_t ny, const float* win, int32_t nfft, float scale, int32_t shift,
-                          float* sxx, int64_t nframes);
-
-/* ---- streaming correlation with a fixed template p of length L (<= 8192):
+/* ---- streaming correlation with a fixed template p of L samples (any L >= 1;
+ * L > 8192 runs as one pass per 8192-sample chunk, accumulated in c):
  * c[o] = sum_{k<L} s[o - off + k] conj(p[k]), mode VALID (off = 0, nout = n-L+1)
  * or FULL (off = L-1, nout = n+L-1).  c may be NULL (peak only).  peak_dev: a
- * device vsig_peak (may be NULL); peak = max |c|, sums over all nout outputs. */
-int vsig_xcorr_create(vsig_ctx* ctx, const void* tmpl, int32_t L, vsig_xcorr** out);
+ * device vsig_peak (may be NULL); peak = max |c|, sums over all nout outputs;
+ * the peak / index are refined (see "refine" above). */
+int vsig_xcorr_create(vsig_ctx* ctx, const void* tmpl, int64_t L, vsig_xcorr** out);
 void vsig_xcorr_free(vsig_xcorr* xc);
 int vsig_xcorr_exec_dev(vsig_xcorr* xc, const void* s, int64_t n, int32_t mode, void* c,
                         vsig_peak_t* peak_dev);
 
 /* ---- general correlation, np.correlate(a, v, mode) semantics for any length
- * order: output length full na+nv-1, valid |na-nv|+1, same max(na, nv).  The
- * shorter operand up to 8192 samples runs as one streaming pass; longer ones
- * as a sum over 8192-sample chunks of it (one pass per chunk, accumulated in
- * c -- a device scratch c when c is NULL).  All pointers device (dev) or host. */
+ * order (cross_correlate_signals, utils.py:1279-1285): output length full
+ * na+nv-1, valid |na-nv|+1, same max(na, nv).  The FFT pass runs in complex64;
+ * dtype VSIG_DTYPE_C128 takes complex128 operands (converted for the FFT pass,
+ * kept for the refine pass), out_dtype VSIG_DTYPE_C128 writes c as complex128
+ * with the refined outputs patched in (exact near the peak, fp32 accuracy
+ * elsewhere).  The shorter operand up to 8192 samples runs as one streaming
+ * pass; longer ones as a sum over 8192-sample chunks of it (one pass per
+ * chunk, accumulated in c -- a device scratch c when c is NULL).  All pointers
+ * device (dev) or host.  The _c64 forms are dtype = out_dtype = C64. */
+int vsig_correlate_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t na, const void* v,
+                       int64_t nv, int32_t mode, int32_t out_dtype, void* c, vsig_peak_t* peak_dev);
+int vsig_correlate(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t na, const void* v,
+                   int64_t nv, int32_t mode, int32_t out_dtype, void* c, vsig_peak_t* peak);
 int vsig_correlate_c64_dev(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,
                            int32_t mode, void* c, vsig_peak_t* peak_dev);
 int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,
@@ -216,7 +218,8 @@ int vsig_pfb_c64_dev(vsig_ctx* ctx, const void* x, int64_t n, const float* h, in
  *   in double (x of any VSIG_DTYPE; sm: max(n, w) doubles on the device).
  * vsig_db_dev: out = 10 log10(|a| + floor), F32 -> float32 math and output,
  *   F64 -> double (numpy's promotion in normalize_spectrogram).
- * vsig_abs_c64_dev: out = |a| + 0j as complex64 (a of any VSIG_DTYPE). */
+ * vsig_abs_c64_dev / vsig_abs_c128_dev: out = |a| + 0j as complex64 / complex128
+ *   (a of any VSIG_DTYPE; np.abs as numpy forms it). */
 int vsig_select_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, const int64_t* ranks,
                     int32_t nranks, double* values);
 int vsig_threshold_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, double thr,
@@ -225,6 +228,7 @@ int vsig_boxcar_energy_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t 
                            double* sm);
 int vsig_db_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, double floor_, void* out);
 int vsig_abs_c64_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, void* out);
+int vsig_abs_c128_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, void* out);
 
 #ifdef __cplusplus
 }

@@ -337,6 +337,64 @@ def transplant_packet_in_vector(vector, packet_signal, vector_location, packet_l
     return new_vector
 
 
+def resample_signal(signal, orig_sr, target_sr):
+    """utils.py:107-118: scipy.signal.resample(signal, int(len * ratio)) then
+    complex64.  Restated from scipy 1.15.3 ``scipy/signal/_signaltools.py``
+    resample (domain='time', no window): full FFT (scipy.fft, the input's
+    precision), positive bins [0, N//2] and negative bins copied into a
+    num-point spectrum, the Nyquist bin split (upsampling) or folded
+    (downsampling) for even N = min(num, Nx), inverse FFT, times num / Nx.
+    Real input goes through rfft / irfft there; the complex path below gives
+    the same values up to rounding, with the imaginary part set to 0."""
+    import scipy.fft as sp_fft
+    if orig_sr == target_sr:
+        return signal
+    x = np.asarray(signal)
+    num = int(len(x) * (target_sr / orig_sr))
+    Nx = x.shape[0]
+    real = np.isrealobj(x)
+    X = sp_fft.fft(x)
+    Y = np.zeros(num, X.dtype)
+    N = min(num, Nx)
+    nyq = N // 2 + 1
+    Y[:nyq] = X[:nyq]
+    if N > 2:
+        Y[nyq - N:] = X[nyq - N:]
+    if N % 2 == 0:
+        if num < Nx:
+            Y[-N // 2] += X[-N // 2]
+        elif Nx < num:
+            Y[N // 2] *= 0.5
+            Y[num - N // 2] = Y[N // 2]
+    y = sp_fft.ifft(Y) * (float(num) / float(Nx))
+    if real:
+        y = y.real
+    return y.astype(np.complex64)
+
+
+CENTER_FREQ = 5230e6   # vector_analyzer/split_channels.py:7
+
+
+def filter_channel(data, center_freq, sample_rate, bandwidth):
+    """vector_analyzer/split_channels.py:15-44, as written: the frequency axis
+    is np.fft.fftfreq(N, 1/sr) * sr + CENTER_FREQ (the extra * sr is the
+    reference's own, so the brick-wall mask covers ~|bw / 2| * N / sr**2 bins),
+    the masked spectrum's negative half is overwritten by the conjugate mirror
+    of its non-negative half (after fftshift; odd N raises numpy's
+    broadcasting ValueError), inverse FFT, real part (float64)."""
+    n = len(data)
+    freqs = np.fft.fftfreq(n, 1 / sample_rate) * sample_rate + CENTER_FREQ
+    X = np.fft.fft(data)
+    mask = (freqs >= center_freq - bandwidth / 2) & (freqs <= center_freq + bandwidth / 2)
+    F = np.zeros_like(X, dtype=complex)
+    F[mask] = X[mask]
+    neg = np.fft.fftshift(freqs) < CENTER_FREQ
+    pos = np.fft.fftshift(freqs) >= CENTER_FREQ
+    Fs = np.fft.fftshift(F)
+    Fs[neg] = np.conj(np.flip(Fs[pos]))
+    return np.real(np.fft.ifft(np.fft.ifftshift(Fs)))
+
+
 def mat2wv_fields(signal, bNormalize=True):
     """vector_analyzer/mat_to_wv_converter.py:28-50: (interleaved int16 I/Q,
     fRMSdBfs, fPeakPowerdBfs) — the SMU-WV payload and level fields."""
@@ -387,12 +445,12 @@ def chain_chunk_seconds(args):
     (synthesised here: the timing, not the values, is the point) and
     find_correlation_peak.  Returns the seconds the chunk took."""
     import time
-    samples, seed, taps, nfft, tmpl = args
+    samples, seed, taps, nfft, tmpl, decim = args
     h, L = len(taps) - 1, len(tmpl)
-    x = synth_iq(h + samples + L - 1, seed=seed)
+    x = synth_iq(h + samples + (L - 1) * decim, seed=seed)
     t0 = time.perf_counter()
-    y = np.convolve(x, taps)[h: h + samples + L - 1]
-    spectrum(y[:samples], 1.0, "hann", nfft, 0, nfft)
+    y = np.convolve(x, taps)[h: h + samples + (L - 1) * decim][::decim]
+    spectrum(y[:samples // decim], 1.0, "hann", nfft, 0, nfft)
     c, lags = cross_correlate_signals(tmpl, y, "valid")
     find_correlation_peak(c, lags)
     return time.perf_counter() - t0

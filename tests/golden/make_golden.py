@@ -22,6 +22,17 @@ Fixture inventory (SURVEY.md §8(c) golden set G1-G5):
   packet.npz           find_packet_start / detect_packet_bounds /
                        find_packet_location_in_vector results (utils.py:784-825, 1372-1434)
   fir.npz              np.convolve(x, taps)[:N][::D] (no reference FIR: numpy-pinned)
+  tone_transplant.npz  the reference's own tone data (data/fixed_test_vector.mat and
+                       data/packet_{1..6}.mat): cross_correlate_signals +
+                       find_correlation_peak of each packet's first 4096 samples in the
+                       vector (full mode) and, for packets 1 and 3, in their own packet and
+                       find_packet_location_in_vector (utils.py:1258-1342, 1372-1434) --
+                       near-tie argmaxes (top-2 |c| gaps 1e-13 .. 7e-12 relative)
+  stream_ops.npz       apply_frequency_shift (utils.py:120-127), transplant_packet_in_vector
+                       (utils.py:1437-1501), resample_signal (utils.py:107-118)
+  wv.npz               mat2wv's SMU-WV file bytes (vector_analyzer/mat_to_wv_converter.py:7-64)
+                       for a synthetic and the reference's sample_vector.mat, normalised or not
+  channel.npz          filter_channel (vector_analyzer/split_channels.py:15-44)
 """
 from __future__ import annotations
 
@@ -235,7 +246,123 @@ def gen_fir():
     save("fir.npz", **out)
 
 
+def gen_tone_transplant():
+    """The transplant workflow on the reference's own data (unified_gui.py:1105-1131:
+    reference segment = a slice of the packet, located in the vector and in the
+    packet).  Packets are complex128 (the .mat files' own precision), the
+    vector complex64."""
+    vec = np.asarray(sio.loadmat(os.path.join(REF, "data", "fixed_test_vector.mat"))["Y"]).ravel()
+    out = dict(vector=vec)
+    for i in range(1, 7):
+        pk = np.asarray(sio.loadmat(os.path.join(REF, "data", f"packet_{i}.mat"))["Y"]).ravel()
+        seg = refutils.extract_reference_segment(pk, 0, 4096)
+        out[f"seg{i}"] = seg
+        c, lags = refutils.cross_correlate_signals(seg, vec)
+        lag, val, conf = refutils.find_correlation_peak(c, lags)
+        a = np.abs(c)
+        top = np.argsort(a)[::-1][:8]
+        out[f"vec{i}_peak"] = np.array([lag, val, conf], np.float64)
+        out[f"vec{i}_argmax"] = np.int64(np.argmax(a))
+        out[f"vec{i}_top_idx"] = top
+        out[f"vec{i}_top_abs"] = a[top]
+        out[f"vec{i}_sums"] = np.array([a.sum(), (a * a).sum()])
+        if i in (1, 3):
+            out[f"packet{i}"] = pk
+            c, lags = refutils.cross_correlate_signals(seg, pk)
+            a = np.abs(c)
+            out[f"pkt{i}_peak"] = np.array(refutils.find_correlation_peak(c, lags), np.float64)
+            out[f"pkt{i}_argmax"] = np.int64(np.argmax(a))
+            out[f"pkt{i}_nearmax"] = np.int64(np.count_nonzero(a >= a.max() * (1 - 1e-12)))
+            out[f"loc{i}"] = np.array(refutils.find_packet_location_in_vector(vec, pk, seg),
+                                      np.float64)
+    save("tone_transplant.npz", **out)
+
+
+def gen_stream_ops():
+    import contextlib
+    import io
+    out = {}
+    x = synth_iq(20_000, seed=21)
+    for j, (f, sr) in enumerate(((1e6, 56e6), (-13.37e6, 56e6), (0.25e6, 1e6))):
+        out[f"shift{j}_args"] = np.array([f, sr])
+        out[f"shift{j}"] = refutils.apply_frequency_shift(x, f, sr)
+    out["shift_x"] = x
+    # transplant_packet_in_vector: the reference's real packet into a synthetic vector
+    pk = np.asarray(sio.loadmat(os.path.join(REF, "data", "packet_3_bpsk.mat"))["Y"]).ravel()
+    pk = pk[:6000].astype(np.complex64)
+    vec = synth_iq(20_000, seed=22)
+    out["tp_packet"], out["tp_vector"] = pk, vec
+    cases = [dict(vector_location=1000), dict(vector_location=17_000),
+             dict(vector_location=200, packet_location=100, replace_length=3000),
+             dict(vector_location=5000, normalize_power=False)]
+    for j, kw in enumerate(cases):
+        with contextlib.redirect_stdout(io.StringIO()):
+            out[f"tp{j}"] = refutils.transplant_packet_in_vector(vec, pk, **kw)
+        out[f"tp{j}_args"] = np.array([kw.get("vector_location"), kw.get("packet_location", 0),
+                                       kw.get("replace_length", -1),
+                                       int(kw.get("normalize_power", True))])
+    # resample_signal: scipy.signal.resample(x, int(len * ratio)).astype(complex64)
+    rs = {"rs0": (synth_iq(10_000, seed=23), 56e6, 40e6), "rs1": (synth_iq(4096, seed=24), 10e6, 25e6),
+          "rs2": (synth_iq(20_001, seed=25), 61.44e6, 56e6), "rs3": (pk[:4_321], 56e6, 56e6 * 1.5),
+          "rs4": (synth_iq(1 << 15, seed=26), 56e6, 14e6)}
+    for k, (sig, a, b) in rs.items():
+        out[f"{k}_x"] = sig
+        out[f"{k}_sr"] = np.array([a, b])
+        out[k] = refutils.resample_signal(sig, a, b)
+    save("stream_ops.npz", **out)
+
+
+def gen_wv(tmpdir="/tmp"):
+    import contextlib
+    import io
+    sys.path.insert(0, os.path.join(REF, "vector_analyzer"))
+    import mat_to_wv_converter as m2w
+    out = {}
+    sv = np.asarray(sio.loadmat(os.path.join(REF, "sample_vector.mat"))["Y"]).ravel()
+    for j, (sig, sr, norm) in enumerate(((synth_iq(3000, seed=31) * 0.3, 56e6, True),
+                                         (synth_iq(3000, seed=32) * 0.3, 61.44e6, False),
+                                         (sv, 56e6, True))):
+        fn = os.path.join(tmpdir, f"golden_wv_{j}.wv")
+        with contextlib.redirect_stdout(io.StringIO()):
+            m2w.mat2wv(sig, fn, sr, bNormalize=norm)
+        out[f"x{j}"] = sig
+        out[f"args{j}"] = np.array([sr, int(norm)])
+        out[f"bytes{j}"] = np.frombuffer(open(fn, "rb").read(), np.uint8)
+        os.remove(fn)
+    save("wv.npz", **out)
+
+
+def gen_channel():
+    sys.path.insert(0, os.path.join(REF, "vector_analyzer"))
+    import split_channels as sc
+    out = {}
+    cases = [(synth_iq(1 << 14, seed=41), 5220e6, 56e6, 20e6),
+             (synth_iq(12_000, seed=42), 5240e6, 56e6, 20e6),
+             (synth_iq(4096, seed=43), 5230e6 - 300.0, 1000.0, 20e6),      # wide mask (small rate)
+             (synth_iq(10_002, seed=44), 5230e6 + 2e6, 2000.0, 6e6)]
+    pk = np.asarray(sio.loadmat(os.path.join(REF, "data", "packet_3_bpsk.mat"))["Y"]).ravel()
+    cases.append((pk[:16_384], 5220e6, 56e6, 20e6))
+    for j, (x, cf, sr, bw) in enumerate(cases):
+        out[f"x{j}"] = x
+        out[f"args{j}"] = np.array([cf, sr, bw])
+        out[f"y{j}"] = sc.filter_channel(x, cf, sr, bw)
+    try:
+        sc.filter_channel(synth_iq(1001, seed=45), 5220e6, 56e6, 20e6)
+        out["odd_raises"] = np.array("")
+    except ValueError as e:
+        out["odd_raises"] = np.array(type(e).__name__)
+    save("channel.npz", **out)
+
+
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()[f"gen_{name}"]()
+        sys.exit(0)
+    gen_tone_transplant()
+    gen_stream_ops()
+    gen_wv()
+    gen_channel()
     gen_spec_params()
     gen_spec_outputs()
     gen_stft()

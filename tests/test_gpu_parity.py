@@ -288,79 +288,53 @@ def test_correlator_stream_full_size_property(gpu):
     assert peak == pytest.approx(direct, rel=1e-5)
 
 
-@pytest.mark.parametrize("variant", [0, 1, 2, 4, 8, 10, 16, 18, 32, 40, 64, 65, 72, 96, 128, 192, 193, 224])
-def test_kernel_variants_agree_with_oracle(gpu, variant):
-    """Every tuning variant (persistent / LDS twiddles / split exchange /
-    512-thread 16k plan) must give the same results as the oracle."""
-    ctx = gpu.get_context()
-    rng = np.random.default_rng(variant)
-    x = ref.synth_iq(3 * 16384 + 77, seed=variant)
-    taps = rng.standard_normal(255).astype(np.float32)
-    tmpl = ref.qpsk_preamble(4096, seed=variant)
-    keys = ("psd_variant", "fir_variant", "xcorr_variant", "fir_m", "xcorr_m")
-    saved = {}
-    for k in keys:
-        v = C.c_int()
-        ctx.check(ctx.lib.vsig_get_option(ctx.h, k.encode(), C.byref(v)), k)
-        saved[k] = v.value
-    try:
-        for k in ("psd_variant", "fir_variant", "xcorr_variant"):
-            ctx.check(ctx.lib.vsig_set_option(ctx.h, k.encode(), variant), k)
-        for m in (4096, 8192, 16384):
-            ctx.check(ctx.lib.vsig_set_option(ctx.h, b"fir_m", m), "fir_m")
-            gpu.dsp._fir_cache.clear()
-            assert_normwise(gpu.filter(x, taps, 1), ref.fir_filter(x, taps, 1), FIR_TOL)
-            assert_normwise(gpu.filter(x, taps, 3), ref.fir_filter(x, taps, 3), FIR_TOL)
-        for nfft in (1024, 4096, 8192, 16384):
-            _, _, S = gpu.spectrum(x, 1.0, "hann", nfft, nfft // 4, nfft)
-            _, _, R = ref.spectrum(x, 1.0, "hann", nfft, nfft // 4, nfft)
-            assert_spectra_close(S, R)
-        for m in (8192, 16384):
-            ctx.check(ctx.lib.vsig_set_option(ctx.h, b"xcorr_m", m), "xcorr_m")
-            c, _ = gpu.cross_correlate_signals(tmpl, x, "valid")
-            r, _ = ref.cross_correlate_signals(tmpl, x, "valid")
-            assert_normwise(c, r, XC_TOL)
-        # streaming Correlator (partitioned when variant bit 5), valid and full
-        import torch
-        s = torch.from_numpy(x).cuda()
-        for L in (4096, 3000, 1500):
-            xc = gpu.Correlator(tmpl[:L])
-            for mode in ("valid", "full"):
-                nout = len(x) - L + 1 if mode == "valid" else len(x) + L - 1
-                out = torch.empty(nout, dtype=torch.complex64, device="cuda")
-                _, pk = xc(s, mode, out=out)
-                r, _ = ref.cross_correlate_signals(tmpl[:L], x, mode)
-                assert_normwise(out.cpu().numpy(), r, XC_TOL)
-                peak, idx, s1, s2 = gpu.dsp._read_peak(pk)
-                a = np.abs(r)
-                assert idx == int(np.argmax(a))
-                assert peak == pytest.approx(a.max(), rel=1e-5)
-                assert s1 == pytest.approx(a.sum(), rel=1e-5)
-    finally:
-        for k, v in saved.items():
-            ctx.lib.vsig_set_option(ctx.h, k.encode(), v)
-        gpu.dsp._fir_cache.clear()
+@pytest.mark.parametrize("ntaps", [255, 300, 1000, 3000])
+def test_fir_block_sizes_agree_with_oracle(gpu, ntaps):
+    """Every overlap-save FIR block size the library plans (M = 1024 / 4096 /
+    8192 / 16384 for these tap counts) against np.convolve, D = 1 and 3."""
+    rng = np.random.default_rng(ntaps)
+    x = ref.synth_iq(3 * 16384 + 77, seed=ntaps)
+    taps = rng.standard_normal(ntaps).astype(np.float32)
+    assert_normwise(gpu.filter(x, taps, 1), ref.fir_filter(x, taps, 1), FIR_TOL)
+    assert_normwise(gpu.filter(x, taps, 3), ref.fir_filter(x, taps, 3), FIR_TOL)
+
+
+@pytest.mark.parametrize("L", [1000, 1500, 3000, 4096])
+def test_correlator_block_sizes_agree_with_oracle(gpu, L):
+    """Correlator block sizes M = 4096 / 8192 / 16384 (L <= 1024 / 2048 /
+    8192): general correlation and the streaming Correlator in valid and full
+    mode, c stored (out=) and the fused peak record (exact argmax)."""
+    import torch
+    x = ref.synth_iq(3 * 16384 + 77, seed=L)
+    tmpl = ref.qpsk_preamble(L, seed=L)
+    c, _ = gpu.cross_correlate_signals(tmpl, x, "valid")
+    r, _ = ref.cross_correlate_signals(tmpl, x, "valid")
+    assert_normwise(c, r, XC_TOL)
+    s = torch.from_numpy(x).cuda()
+    xc = gpu.Correlator(tmpl)
+    for mode in ("valid", "full"):
+        nout = len(x) - L + 1 if mode == "valid" else len(x) + L - 1
+        out = torch.empty(nout, dtype=torch.complex64, device="cuda")
+        _, pk = xc(s, mode, out=out)
+        r, _ = ref.cross_correlate_signals(tmpl, x, mode)
+        assert_normwise(out.cpu().numpy(), r, XC_TOL)
+        peak, idx, s1, s2 = gpu.dsp._read_peak(pk)
+        a = np.abs(r)
+        assert idx == int(np.argmax(a))
+        assert peak == pytest.approx(a.max(), rel=1e-12)   # refined: fp64 direct sum
+        assert s1 == pytest.approx(a.sum(), rel=1e-5)
 
 
 @pytest.mark.parametrize("decim", [2, 3, 4])
 @pytest.mark.parametrize("n", [1, 777, 100_003, 3 * 16384 + 77])
-def test_decimating_fir_frequency_domain(gpu, decim, n):
-    """fir_variant bit 8: decimation folded into the spectrum (M/D-point
-    inverse transforms) for D = 2 / 4 (D = 3 falls back to the full-rate
-    kernel); same outputs as np.convolve(x, h)[:n][::D], any length."""
-    ctx = gpu.get_context()
-    v = C.c_int()
-    ctx.check(ctx.lib.vsig_get_option(ctx.h, b"fir_variant", C.byref(v)), "get")
+def test_decimating_fir(gpu, decim, n):
+    """Decimation folded into the spectrum (M/D-point inverse transforms) for
+    D = 2 / 4, the full-rate kernel with the decimating store for D = 3; same
+    outputs as np.convolve(x, h)[:n][::D], any length."""
     rng = np.random.default_rng(n + decim)
     x = ref.synth_iq(n, seed=n)
     for taps in (rng.standard_normal(255).astype(np.float32), np.hanning(65)[1:-1].astype(np.float32)):
-        try:
-            ctx.check(ctx.lib.vsig_set_option(ctx.h, b"fir_variant", v.value | 256), "set")
-            gpu.dsp._fir_cache.clear()
-            assert_normwise(gpu.filter(x, taps, decim), ref.fir_filter(x, taps, decim), FIR_TOL)
-        finally:
-            ctx.lib.vsig_set_option(ctx.h, b"fir_variant", v.value)
-            gpu.dsp._fir_cache.clear()
+        assert_normwise(gpu.filter(x, taps, decim), ref.fir_filter(x, taps, decim), FIR_TOL)
 
 
 @pytest.mark.parametrize("l1,l2", [(20_000, 61_234), (61_234, 20_000), (8193, 30_000),

@@ -124,3 +124,66 @@ def test_synthetic_generators_deterministic():
     np.testing.assert_array_equal(a, b)
     p = ref.qpsk_preamble(64)
     np.testing.assert_allclose(np.abs(p), 1.0, rtol=1e-6)
+
+
+# ---------------------------------------------------------------- round-2 fixtures
+def test_tone_transplant_oracle():
+    """The reference's own tone data (data/packet_*.mat in data/fixed_test_vector.mat):
+    the oracle's argmax, peak and confidence equal the reference's bit for bit."""
+    g = golden("tone_transplant.npz")
+    vec = g["vector"]
+    for i in range(1, 7):
+        seg = g[f"seg{i}"]
+        c, lags = ref.cross_correlate_signals(seg, vec)
+        assert int(np.argmax(np.abs(c))) == int(g[f"vec{i}_argmax"])
+        np.testing.assert_array_equal(np.array(ref.find_correlation_peak(c, lags), np.float64),
+                                      g[f"vec{i}_peak"])
+    for i in (1, 3):
+        pk, seg = g[f"packet{i}"], g[f"seg{i}"]
+        c, lags = ref.cross_correlate_signals(seg, pk)
+        assert int(np.argmax(np.abs(c))) == int(g[f"pkt{i}_argmax"])
+        np.testing.assert_array_equal(
+            np.array(ref.find_packet_location_in_vector(vec, pk, seg), np.float64), g[f"loc{i}"])
+
+
+def test_stream_ops_oracle():
+    g = golden("stream_ops.npz")
+    x = g["shift_x"]
+    for j in range(3):
+        f, sr = g[f"shift{j}_args"]
+        np.testing.assert_array_equal(ref.apply_frequency_shift(x, f, sr), g[f"shift{j}"])
+    for j in range(4):
+        vl, pl, rl, npow = (int(v) for v in g[f"tp{j}_args"])
+        out = ref.transplant_packet_in_vector(g["tp_vector"], g["tp_packet"], vl, pl,
+                                              None if rl < 0 else rl, bool(npow))
+        np.testing.assert_array_equal(out, g[f"tp{j}"])
+    for j in range(5):
+        a, b = g[f"rs{j}_sr"]
+        y = ref.resample_signal(g[f"rs{j}_x"], a, b)
+        assert y.dtype == np.complex64 and y.shape == g[f"rs{j}"].shape
+        np.testing.assert_array_equal(y, g[f"rs{j}"])
+
+
+def test_wv_oracle():
+    """mat2wv's payload and level fields from the oracle against the bytes of the
+    file the reference wrote (everything but its DATE field)."""
+    g = golden("wv.npz")
+    for j in range(3):
+        sr, norm = g[f"args{j}"]
+        raw = g[f"bytes{j}"].tobytes()
+        payload, rms, peak = ref.mat2wv_fields(g[f"x{j}"], bool(norm))
+        head = raw[: raw.index(b"#") + 1]
+        assert raw[len(head):] == payload.tobytes() + b"}"
+        assert f"{{LEVEL OFFS: {rms}, {peak}}}".encode() in head
+        assert f"{{CLOCK: {sr}}}".encode() in head
+        assert f"{{SAMPLES: {len(g[f'x{j}'])}}}".encode() in head
+
+
+def test_channel_oracle():
+    g = golden("channel.npz")
+    for j in range(5):
+        cf, sr, bw = g[f"args{j}"]
+        np.testing.assert_array_equal(ref.filter_channel(g[f"x{j}"], cf, sr, bw), g[f"y{j}"])
+    assert str(g["odd_raises"]) == "ValueError"
+    with pytest.raises(ValueError):
+        ref.filter_channel(ref.synth_iq(1001, seed=45), 5220e6, 56e6, 20e6)

@@ -63,7 +63,7 @@ def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None, 
 
 
 def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, serial=False,
-            fuse=False, freq_shift=0.0):
+            freq_shift=0.0):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -71,7 +71,7 @@ def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, se
         x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L,
                                         freq_shift=freq_shift)
         cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre,
-                          pipeline=pipeline, serial=serial, fuse=fuse, freq_shift=freq_shift,
+                          pipeline=pipeline, serial=serial, freq_shift=freq_shift,
                           sample_rate=SR)
         be = OracleBackend(cfg)
 
@@ -88,18 +88,9 @@ def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, se
                 if a < b:
                     y[a - lo:b - lo] += torch.from_numpy((6 * pre[a - k0:b - k0]).astype(np.complex64))
 
-            def can_fuse(self, cfg):
-                return fuse
-
-            def fir_psd_into(self, x_ext, nhist, y, sxx):
-                # the fused launch's contract: FIR then the PSD of its output
-                self.fir_into(x_ext, nhist, y)
-                self.psd_into(y, sxx)
-
         ch_holder = []
         be = PlantingBackend(cfg)
         ch = StreamChain(cfg, be, rank, world)
-        assert ch.fused == (fuse and decim == 1 and pipeline == 1 and not serial)
         ch_holder.append(ch)
         ch.x.copy_(torch.from_numpy(x[rank * n_local:(rank + 1) * n_local]))
         ch.step()
@@ -116,22 +107,23 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,pipeline,serial,fuse,freq_shift", [
-    (2, 1, False, False, 0.0), (3, 1, False, False, 0.0), (2, 4, False, False, 0.0),
-    (1, 4, False, False, 0.0), (2, 4, True, False, 0.0), (3, 2, True, False, 0.0),
-    (2, 1, False, True, 0.0), (3, 1, False, True, 0.0), (1, 1, False, True, 0.0),
-    (3, 1, False, False, FS), (2, 4, True, False, FS)])
-def test_sharded_chain_matches_single_stream(world, pipeline, serial, fuse, freq_shift):
-    """fuse: the fused FIR + PSD launch (decim 1), split at a frame boundary on
-    ranks > 0 so the bulk runs while the left halo is in flight.  freq_shift:
-    the mixer before the FIR, phase from the global sample index on every rank."""
-    n_local, decim, nfft, ntaps, L = 4096, 1 if fuse else 2, 256, 31, 100
+@pytest.mark.parametrize("world,pipeline,serial,decim,L,freq_shift", [
+    (2, 1, False, 2, 100, 0.0), (3, 1, False, 2, 100, 0.0), (2, 4, False, 2, 100, 0.0),
+    (1, 4, False, 2, 100, 0.0), (2, 4, True, 2, 100, 0.0), (3, 2, True, 2, 100, 0.0),
+    (2, 1, False, 1, 100, 0.0), (3, 1, False, 1, 300, 0.0), (2, 4, False, 1, 450, 0.0),
+    (3, 1, False, 2, 100, FS), (2, 4, True, 2, 100, FS)])
+def test_sharded_chain_matches_single_stream(world, pipeline, serial, decim, L, freq_shift):
+    """decim 1: the left halo's split at ntaps-1 outputs; long templates (L up
+    to 450, a sub-chunk of 512 filtered samples at pipeline 4) widen the right
+    halo.  freq_shift: the mixer before the FIR, phase from the global sample
+    index on every rank."""
+    n_local, nfft, ntaps = 4096, 256, 31
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_worker,
                          args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline, serial,
-                               fuse, freq_shift))
+                               freq_shift))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -2,12 +2,14 @@
 import os, sys, json
 import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _tune  # noqa: E402,F401  (libvsig_tune.so)
 import vector_amd as va
 from vector_amd import dsp
 ctx = va.get_context(0)
 ctx.bind_stream()
 iters = 20
-for key in (-1024, -2048, 4096, 8192, 16384, -16384):
+for key in (-1024, 4096, 8192, 16384):
     N = abs(key)
     frames = max(1, (1 << 28) // N // 8)      # 2**25 points per launch
     io = torch.randn(frames * N, dtype=torch.complex64, device="cuda")

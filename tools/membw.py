@@ -8,6 +8,8 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import _tune  # noqa: E402,F401  (libvsig_tune.so)
 n = 1 << 28
 x = torch.randn(n, dtype=torch.complex64, device="cuda")
 y = torch.empty_like(x)

@@ -38,6 +38,8 @@ I32, I64, F32 = C.c_int32, C.c_int64, C.c_float
 # name -> (restype, argtypes); every symbol include/vsig.h declares.
 SIGNATURES = {
     "vsig_version": (C.c_int, []),
+    "vsig_build_id": (C.c_char_p, []),
+    "vsig_refine_status": (C.c_int, [P, C.POINTER(I32), C.POINTER(I64)]),
     "vsig_errstr": (C.c_char_p, [C.c_int]),
     "vsig_init": (C.c_int, [C.c_int, C.POINTER(P)]),
     "vsig_free": (None, [P]),
@@ -46,8 +48,6 @@ SIGNATURES = {
     "vsig_synchronize": (C.c_int, [P]),
     "vsig_set_option": (C.c_int, [P, C.c_char_p, C.c_int]),
     "vsig_get_option": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
-    "vsig_copy_bench": (C.c_int, [P, P, I64, P, C.c_int, C.c_int]),
-    "vsig_fft_bench": (C.c_int, [P, C.c_int, P, C.c_int, C.c_int, C.c_int]),
     "vsig_timing_enable": (C.c_int, [P, C.c_int]),
     "vsig_timing_read": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(I64)]),
     "vsig_timing_reset": (C.c_int, [P]),
@@ -60,10 +60,11 @@ SIGNATURES = {
     "vsig_fir_c64": (C.c_int, [P, P, I64, P, I32, I32, P, I64]),
     "vsig_fir_block": (C.c_int, [P]),
     "vsig_fir_exec_mix_dev": (C.c_int, [P, P, I64, I64, P, I64, C.c_double, C.c_double, I64]),
-    "vsig_fir_psd_exec_dev": (C.c_int, [P, P, I64, I64, P, I64, P, I32, F32, I32, P, I64]),
-    "vsig_xcorr_create": (C.c_int, [P, P, I32, C.POINTER(P)]),
+    "vsig_xcorr_create": (C.c_int, [P, P, I64, C.POINTER(P)]),
     "vsig_xcorr_free": (None, [P]),
     "vsig_xcorr_exec_dev": (C.c_int, [P, P, I64, I32, P, P]),
+    "vsig_correlate_dev": (C.c_int, [P, I32, P, I64, P, I64, I32, I32, P, P]),
+    "vsig_correlate": (C.c_int, [P, I32, P, I64, P, I64, I32, I32, P, P]),
     "vsig_correlate_c64_dev": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
     "vsig_correlate_c64": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
     "vsig_peak_dev": (C.c_int, [P, I32, P, I64, P]),
@@ -80,6 +81,7 @@ SIGNATURES = {
     "vsig_boxcar_energy_dev": (C.c_int, [P, I32, P, I64, I64, P]),
     "vsig_db_dev": (C.c_int, [P, I32, P, I64, C.c_double, P]),
     "vsig_abs_c64_dev": (C.c_int, [P, I32, P, I64, P]),
+    "vsig_abs_c128_dev": (C.c_int, [P, I32, P, I64, P]),
 }
 
 _lib = None
@@ -88,7 +90,9 @@ _lib_lock = threading.Lock()
 
 def load_library(path: str | None = None):
     """Load libvsig.so and declare every entry point; no device needed.
-    (VSIG_LIB selects an A/B build of the same sources, for the tuning tools.)"""
+    (VSIG_LIB selects an A/B build of the same sources, for the tuning tools.)
+    The library's build id must equal the hash of the kernel sources next to
+    it (vector_amd/csrc, include/vsig.h): a stale binary is refused."""
     global _lib
     path = path or os.environ.get("VSIG_LIB") or LIB_PATH
     with _lib_lock:
@@ -103,6 +107,11 @@ def load_library(path: str | None = None):
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        from ._build import source_hash
+        want, got = source_hash(), lib.vsig_build_id().decode()
+        if want is not None and got != want:
+            raise VsigUnavailable(f"{path} was built from other sources (build id {got}, sources "
+                                  f"{want}): rebuild with `python -m vector_amd._build`")
         _lib = lib
         return lib
 

@@ -284,12 +284,16 @@ def find_packet_start(signal, template=None, threshold_ratio=0.2, window_size=No
         tm, tcode = _to_device(template, ctx)
         if s.numel() == 0 or tm.numel() == 0:
             raise ValueError("v cannot be empty" if tm.numel() == 0 else "a cannot be empty")
-        sa = torch.empty(int(s.numel()), dtype=torch.complex64, device=s.device)
-        ta = torch.empty(int(tm.numel()), dtype=torch.complex64, device=s.device)
-        ctx.check(ctx.lib.vsig_abs_c64_dev(ctx.h, _lib.DTYPES[scode], _ptr(s), int(s.numel()),
-                                           _ptr(sa)), "abs")
-        ctx.check(ctx.lib.vsig_abs_c64_dev(ctx.h, _lib.DTYPES[tcode], _ptr(tm), int(tm.numel()),
-                                           _ptr(ta)), "abs")
+        # np.abs keeps the input's precision: complex64 / float32 magnitudes are
+        # float32 (exact in complex64), wider ones float64 (complex128 operands
+        # of the correlation, so the argmax refine sees numpy's values)
+        wide = scode in ("c128", "f64") or tcode in ("c128", "f64")
+        odt = torch.complex128 if wide else torch.complex64
+        absfn = ctx.lib.vsig_abs_c128_dev if wide else ctx.lib.vsig_abs_c64_dev
+        sa = torch.empty(int(s.numel()), dtype=odt, device=s.device)
+        ta = torch.empty(int(tm.numel()), dtype=odt, device=s.device)
+        ctx.check(absfn(ctx.h, _lib.DTYPES[scode], _ptr(s), int(s.numel()), _ptr(sa)), "abs")
+        ctx.check(absfn(ctx.h, _lib.DTYPES[tcode], _ptr(tm), int(tm.numel()), _ptr(ta)), "abs")
         _, pk, _ = _correlate_dev(sa, ta, "valid", False, ctx)
         return int(pk.cpu().view(torch.int64)[1].item())
     t, code = _to_device(signal, ctx)

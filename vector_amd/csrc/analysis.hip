@@ -269,28 +269,21 @@ __global__ __launch_bounds__(256) void db_transform_f32(const float* __restrict_
     out[i] = __fmul_rn(10.f, (float)log10((double)__fadd_rn(fabsf(a[i]), floor_)));
 }
 
-template <class T>
-__global__ __launch_bounds__(256) void abs_to_c64(const T* __restrict__ a, long long n,
-                                                  float2* __restrict__ out) {
-  const long long stride = (long long)gridDim.x * 256;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-    const T v = a[i];
-    out[i] = make_float2((float)cabs_np(v.x, v.y), 0.f);
-  }
-}
-template <>
-__global__ __launch_bounds__(256) void abs_to_c64<double>(const double* __restrict__ a, long long n,
-                                                          float2* __restrict__ out) {
-  const long long stride = (long long)gridDim.x * 256;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
-    out[i] = make_float2((float)fabs(a[i]), 0.f);
-}
-template <>
-__global__ __launch_bounds__(256) void abs_to_c64<float>(const float* __restrict__ a, long long n,
-                                                         float2* __restrict__ out) {
+// |a| + 0j (np.abs as numpy computes it: complex -> cabs_np, real -> fabs),
+// written as complex64 (O = float2) or complex128 (O = double2).
+template <class T> __device__ __forceinline__ double absd(const T& v) { return cabs_np(v.x, v.y); }
+template <> __device__ __forceinline__ double absd<double>(const double& v) { return fabs(v); }
+template <> __device__ __forceinline__ double absd<float>(const float& v) { return (double)fabsf(v); }
+template <class O> __device__ __forceinline__ O mk_re(double r);
+template <> __device__ __forceinline__ float2 mk_re<float2>(double r) { return make_float2((float)r, 0.f); }
+template <> __device__ __forceinline__ double2 mk_re<double2>(double r) { return make_double2(r, 0.0); }
+
+template <class T, class O>
+__global__ __launch_bounds__(256) void abs_to_c(const T* __restrict__ a, long long n,
+                                                O* __restrict__ out) {
   const long long stride = (long long)gridDim.x * 256;
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride)
-    out[i] = make_float2(fabsf(a[i]), 0.f);
+    out[i] = mk_re<O>(absd<T>(a[i]));
 }
 
 // ---------------------------------------------------------------- launchers
@@ -370,16 +363,23 @@ hipError_t launch_db_transform(int dtype, const void* a, long long n, double flo
   return hipGetLastError();
 }
 
-hipError_t launch_abs_c64(int dtype, const void* a, long long n, float2* out, hipStream_t st) {
+template <class O>
+static hipError_t launch_abs_t(int dtype, const void* a, long long n, O* out, hipStream_t st) {
   const int g = grid_for(n);
   switch (dtype) {
-    case VSIG_C128: hipLaunchKernelGGL(abs_to_c64<double2>, dim3(g), dim3(256), 0, st, (const double2*)a, n, out); break;
-    case VSIG_C64: hipLaunchKernelGGL(abs_to_c64<float2>, dim3(g), dim3(256), 0, st, (const float2*)a, n, out); break;
-    case VSIG_F64: hipLaunchKernelGGL(abs_to_c64<double>, dim3(g), dim3(256), 0, st, (const double*)a, n, out); break;
-    case VSIG_F32: hipLaunchKernelGGL(abs_to_c64<float>, dim3(g), dim3(256), 0, st, (const float*)a, n, out); break;
+    case VSIG_C128: hipLaunchKernelGGL((abs_to_c<double2, O>), dim3(g), dim3(256), 0, st, (const double2*)a, n, out); break;
+    case VSIG_C64: hipLaunchKernelGGL((abs_to_c<float2, O>), dim3(g), dim3(256), 0, st, (const float2*)a, n, out); break;
+    case VSIG_F64: hipLaunchKernelGGL((abs_to_c<double, O>), dim3(g), dim3(256), 0, st, (const double*)a, n, out); break;
+    case VSIG_F32: hipLaunchKernelGGL((abs_to_c<float, O>), dim3(g), dim3(256), 0, st, (const float*)a, n, out); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+hipError_t launch_abs_c64(int dtype, const void* a, long long n, float2* out, hipStream_t st) {
+  return launch_abs_t<float2>(dtype, a, n, out, st);
+}
+hipError_t launch_abs_c128(int dtype, const void* a, long long n, double2* out, hipStream_t st) {
+  return launch_abs_t<double2>(dtype, a, n, out, st);
 }
 
 }  // namespace vsig

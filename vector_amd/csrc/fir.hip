@@ -41,139 +41,48 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 // The segment x[b*hop - (ntaps-1) .. + M) is FFT'd, multiplied by Hs = FFT(h)/M
 // and inverse-transformed (conj trick), all in LDS / registers.
 // ---------------------------------------------------------------------------
-template <class P, int PERSIST, bool MIX = false>
-__global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void fir_os_kernel(
+// Two consecutive blocks per workgroup (fft_pair: the LDS stores of one
+// segment overlap the other's butterflies), twiddles from register anchors.
+// MIX: the NCO mixer applied to every loaded sample (vsig_fir_exec_mix_dev).
+template <class P, bool MIX = false>
+__global__ __launch_bounds__(P::TF) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
     const float2* __restrict__ tw, MixArgs mix) {
-  static_assert(!MIX || PERSIST == 6, "the fused mixer is built for the pair kernel");
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  constexpr int BT = os_threads<P>();
-  static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[os_lds<P, PERSIST>()];
+  __shared__ float2 lds[P::LDS];
   const int t = threadIdx.x;
-  long long b = PERSIST == 0 || PERSIST >= 3 ? xcd_remap(stage_bid<1>(), gridDim.x) : blockIdx.x;
-  if (b >= nblocks) return;  // uniform per block
-
+  const long long b = xcd_remap(blockIdx.x, gridDim.x);
+  if (2 * b >= nblocks) return;  // uniform per block
   const int lo = ntaps - 1;
   const long long nloc = n - g0;
-  if constexpr (PERSIST == 5) {      // one unit per block, register twiddle anchors
-    float2 wa[nanch_total<P>()];
-    load_anchors<P>(wa, tw, t);
-    float2 v[P::E];
-    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
-    fft_frame_anch<P>(v, lds, wa, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-    fft_frame_anch<P>(v, lds, wa, t);
-    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
-    return;
-  }
-  if constexpr (PERSIST == 6 || PERSIST == 7) {   // two consecutive units per block (fft_pair):
-    // 6: register twiddle anchors; 7: exact per-thread twiddles in registers (TwRegs)
-    constexpr bool RT = PERSIST == 7;
-    float2 wa[RT ? rtw_total<P>() : nanch_total<P>()];
-    if constexpr (RT) load_rtw<P>(wa, tw, t);
-    else load_anchors<P>(wa, tw, t);
-    const long long b0 = 2 * b, b1 = 2 * b + 1;
-    float2 a[P::E], d[P::E];
-    if constexpr (MIX) {
-      load_segment_mix<P>(a, x, g0 + b0 * hop - lo, n, t, mix);
-      load_segment_mix<P>(d, x, g0 + b1 * hop - lo, n, t, mix);
-    } else {
-      load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
-      load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
-    }
-    auto fft2 = [&]() {
-      if constexpr (RT) fft_pair<P>(a, d, lds, TwRegs{wa}, t);
-      else { launder_anchors<P>(wa); fft_pair<P>(a, d, lds, TwAnchors{wa}, t); }
-    };
-    fft2();
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const float2 h = Hs[out_index<P>(t, e)];
-      a[e] = cconj(cmul(a[e], h));
-      d[e] = cconj(cmul(d[e], h));
-    }
-    fft2();
-    fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
-    fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
-    return;
-  }
-  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
-    float2* t2 = lds + (P::LDS + 1) / 2;
-    float* ldf = reinterpret_cast<float*>(lds);
-    load_tw2<P>(t2, tw, t, BT);
-    float2 v[P::E];
-    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
-    fft_frame_split<P>(v, ldf, t2, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-    fft_frame_split<P>(v, ldf, t2, t);
-    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
-    return;
-  }
-  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
-    float2* t2 = lds + P::LDS;
-    load_tw2<P>(t2, tw, t, BT);
-    float2 v[P::E];
-    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
-    fft_frame_t2<P>(v, lds, t2, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-    fft_frame_t2<P>(v, lds, t2, t);
-    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
-    return;
-  }
-  if constexpr (!PERSIST) {          // one unit per block, table twiddles
-    float2 v[P::E];
-    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
-    fft_frame<P>(v, lds, tw, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-    fft_frame<P>(v, lds, tw, t);
-    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
-    return;
-  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
-    float2 v[P::E];
-    load_segment<P>(v, x, g0 + b * hop - lo, n, t);
-    for (; b < nblocks; b += gridDim.x) {
-      fft_frame<P>(v, lds, tw, t);
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-      float2 nv[P::E];
-      const long long nb = b + gridDim.x;
-      fft_frame_hook<P>(v, lds, tw, t, [&] {
-        if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
-      });
-      fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
-    }
-    return;
-  }
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
-  float2 v[P::E];
-  load_segment<P>(v, x, g0 + b * hop - lo, n, t);
-  for (; b < nblocks; b += gridDim.x) {
-    fft_frame_anch<P>(v, lds, wa, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cconj(cmul(v[e], Hs[out_index<P>(t, e)]));
-    // Prefetch after the (L2-resident) filter-spectrum loads: vmcnt retires in
-    // issue order, so the next segment then lands behind the inverse FFT.
-    float2 nv[P::E];
-    const long long nb = b + gridDim.x;
-    if (nb < nblocks) load_segment<P>(nv, x, g0 + nb * hop - lo, n, t);
-    fft_frame_anch<P>(v, lds, wa, t);
-    fir_store<P>(v, y, b, hop, lo, nloc, decim, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = nv[e];
+  const long long b0 = 2 * b, b1 = 2 * b + 1;
+  float2 a[P::E], d[P::E];
+  if constexpr (MIX) {
+    load_segment_mix<P>(a, x, g0 + b0 * hop - lo, n, t, mix);
+    load_segment_mix<P>(d, x, g0 + b1 * hop - lo, n, t, mix);
+  } else {
+    load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
+    load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
   }
+  launder_anchors<P>(wa);
+  fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+#pragma unroll
+  for (int e = 0; e < P::E; ++e) {
+    const float2 h = Hs[out_index<P>(t, e)];
+    a[e] = cconj(cmul(a[e], h));
+    d[e] = cconj(cmul(d[e], h));
+  }
+  launder_anchors<P>(wa);
+  fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+  fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
+  fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
 }
 
 // ---------------------------------------------------------------------------
-// Decimating FIR (variant bit 8), decimation in the frequency domain: after
+// Decimating FIR (D = 2 / 4 at M = 1024), decimation in the frequency domain: after
 // FFT_M(segment) x H/M, only every D-th output of the block is wanted, and
 //   y[D n] = sum_{k' < M/D} Yd[k'] W_{M/D}^{-n k'},  Yd[k'] = sum_{m < D} Y[k' + m M/D],
 // so the inverse transform shrinks to M/D points (PD) after an in-register
@@ -263,39 +172,32 @@ hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0,
   return hipGetLastError();
 }
 
-template <class PL, int PERSIST, bool MIX = false>
-void launch_fir_t(const float2* x, long long n, long long g0, const float2* Hs, int ntaps,
-                  long long hop, int decim, float2* y, long long nblocks, const float2* tw,
-                  hipStream_t st, MixArgs mix = MixArgs{}) {
-  const long long grid =
-      (PERSIST == 1 || PERSIST == 2)
-          ? persistent_grid(fir_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks)
-          : (PERSIST == 6 || PERSIST == 7) ? (nblocks + 1) / 2 : nblocks;
-  hipLaunchKernelGGL((fir_os_kernel<PL, PERSIST, MIX>), dim3((unsigned)grid), dim3(os_threads<PL>()),
-                     0, st, x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, mix);
-}
-
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
-                         int variant, hipStream_t st, const MixArgs* mix) {
+                         hipStream_t st, const MixArgs* mix) {
   if (n - g0 <= 0) return hipSuccess;
   const long long nblocks = (n - g0 + hop - 1) / hop;
-  if (mix) {   // fused mixer: the default one-wave pair kernel (M = 1024) only
-    if ((variant & (8 | 16 | 128)) || !(variant & 64) || M != 1024) return hipErrorInvalidValue;
-    launch_fir_t<Plan1024s, 6, true>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st, *mix);
-    return hipGetLastError();
+  const dim3 grid((unsigned)((nblocks + 1) / 2));
+  const MixArgs m = mix ? *mix : MixArgs{};
+  auto run = [&](auto plan) {
+    using PL = decltype(plan);
+    if constexpr (PL::TF == 64) {
+      if (mix) {
+        hipLaunchKernelGGL((fir_os_kernel<PL, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps,
+                           hop, decim, y, nblocks, tw, m);
+        return;
+      }
+    }
+      hipLaunchKernelGGL((fir_os_kernel<PL, false>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps,
+                         hop, decim, y, nblocks, tw, m);
+  };
+  switch (M) {
+    case 1024: run(Plan1024s{}); break;
+    case 4096: if (mix) return hipErrorInvalidValue; run(Plan4096{}); break;
+    case 8192: if (mix) return hipErrorInvalidValue; run(Plan8192{}); break;
+    case 16384: if (mix) return hipErrorInvalidValue; run(Plan16384{}); break;
+    default: return hipErrorInvalidValue;
   }
-  VSIG_OS_SWITCH(M, variant, {
-    // (bits 3/4 first: they select the two-level twiddle table the API built)
-    if (variant & 16) launch_fir_t<PL, 4>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else if (variant & 8) launch_fir_t<PL, 3>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else if (variant & 128) launch_fir_t<PL, 7>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else if (variant & 64) launch_fir_t<PL, 6>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else if (variant & 32) launch_fir_t<PL, 5>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else if (variant & 4) launch_fir_t<PL, 2>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else if (variant & 1) launch_fir_t<PL, 1>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-    else launch_fir_t<PL, 0>(x, n, g0, Hs, ntaps, hop, decim, y, nblocks, tw, st);
-  });
   return hipGetLastError();
 }
 

@@ -13,47 +13,16 @@ namespace vsig {
 // loads and the FIR's output stores (so the filtered stream does not sit in
 // L2 / the Infinity Cache as dirty lines while the PSD and the correlator
 // read it); the FIR's overlapping segment loads stay plain (NT measured
-// slower there).  VSIG_NT_LD / VSIG_NT_ST force all on (A/B builds).
-#ifndef VSIG_NT_LD
-#define VSIG_NT_LD 0
-#endif
-#ifndef VSIG_NT_ST
-#define VSIG_NT_ST 0
-#endif
+// slower there).
 template <bool NT = false>
 __device__ __forceinline__ float2 ld_stream(const float2* p) {
-  if constexpr (NT || VSIG_NT_LD) return fromv(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
+  if constexpr (NT) return fromv(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
   else return *p;
 }
 template <bool NT = true>
 __device__ __forceinline__ void st_stream(float2* p, float2 v) {
-  if constexpr (NT || VSIG_NT_ST) __builtin_nontemporal_store(tov(v), reinterpret_cast<f2v*>(p));
+  if constexpr (NT) __builtin_nontemporal_store(tov(v), reinterpret_cast<f2v*>(p));
   else *p = v;
-}
-
-template <class P, int PERSIST>
-constexpr int min_waves() {
-#ifdef VSIG_EXP_SPLIT_W4
-  return PERSIST == 4 ? 4 : 1;
-#else
-#ifdef VSIG_EXP_PAIR_W
-  if (PERSIST == 6 && P::TF == 64) return VSIG_EXP_PAIR_W;
-#endif
-  return (PERSIST == 4 && P::E <= 16) ? 4 : 1;
-#endif
-}
-
-// Overlap-save kernels run one frame per block: TF threads (one wave for the
-// 1024 / 2048-point plans, whose barriers then cost nothing).
-template <class P>
-constexpr int os_threads() { return P::TF; }
-
-// LDS (in float2) of a one-frame block: data (halved by the split exchange)
-// plus the two-level twiddle table for variants 3 and 4.
-template <class P, int PERSIST>
-constexpr int os_lds() {
-  return (PERSIST == 4 ? (P::LDS + 1) / 2 : P::LDS) +
-         ((PERSIST == 3 || PERSIST == 4) ? tw2_size<P>() : 0);
 }
 
 // Pass-0 operands of an overlap-save segment x[s0 .. s0 + N) with zero fill
@@ -205,22 +174,6 @@ long long persistent_grid(K kernel, int block, long long units) {
     case 8192: { using PL = Plan8192; __VA_ARGS__; } break;       \
     case 16384: { using PL = Plan16384; __VA_ARGS__; } break;     \
     default: return hipErrorInvalidValue;                  \
-  }
-
-// Only plans with one frame per block can run the overlap-save kernels.
-// variant bit 0: persistent (prefetch + register anchors); bit 1: the E = 32 /
-// 512-thread plan for M = 16384 instead of E = 16 / 1024 threads.
-#define VSIG_OS_SWITCH(N, V, ...)                                          \
-  switch (N) {                                                              \
-    case 1024: { using PL = Plan1024s; __VA_ARGS__; } break;                \
-    case 2048: { using PL = Plan2048s; __VA_ARGS__; } break;                \
-    case 4096: { using PL = Plan4096; __VA_ARGS__; } break;                        \
-    case 8192: { using PL = Plan8192; __VA_ARGS__; } break;                        \
-    case 16384:                                                             \
-      if ((V) & 2) { using PL = Plan16384w; __VA_ARGS__; }                         \
-      else { using PL = Plan16384; __VA_ARGS__; }                                  \
-      break;                                                                \
-    default: return hipErrorInvalidValue;                                   \
   }
 
 }  // namespace vsig

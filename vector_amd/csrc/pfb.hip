@@ -113,38 +113,31 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
   }
 }
 
+// Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3),
+// 64 frames per group.
 template <class PL, int PT>
 static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
-                         const float2* tw, int variant, int fpg_hint, hipStream_t st) {
+                         const float2* tw, hipStream_t st) {
   constexpr int G = 256 / PL::N, E = PL::E;
   constexpr int step = E * (PT / cgcd(E, PT));
-  // frames per group: a multiple of the unrolled step, ~128 frames by default
-  // so the (PT-1)-row ring prologue stays a small fraction of the group's reads
-  const int want = fpg_hint > 0 ? fpg_hint : 128;
+  // frames per group: a multiple of the unrolled step, so the (PT-1)-row ring
+  // prologue stays a small fraction of the group's reads
+  constexpr long long want = 64;
   const long long fpg = ((want + step - 1) / step) * step;
   const long long groups = (M + fpg - 1) / fpg;
   const long long blocks = (groups + G - 1) / G;
-#define VSIG_PFB_GO(V) \
-  hipLaunchKernelGGL((pfb_kernel<PL, PT, V>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M, fpg, y, tw)
-  switch (variant & 7) {
-    case 0: VSIG_PFB_GO(0); break;
-    case 1: VSIG_PFB_GO(1); break;
-    case 2: VSIG_PFB_GO(2); break;
-    case 3: VSIG_PFB_GO(3); break;
-    case 7: VSIG_PFB_GO(7); break;
-    default: VSIG_PFB_GO(3); break;
-  }
-#undef VSIG_PFB_GO
+  hipLaunchKernelGGL((pfb_kernel<PL, PT, 3>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M,
+                     fpg, y, tw);
 }
 
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
-                      float2* y, const float2* tw, int variant, int fpg, hipStream_t st) {
+                      float2* y, const float2* tw, hipStream_t st) {
 #define VSIG_PFB_CASE(CC, PL)                                                        \
   if (C == CC) {                                                                     \
     switch (PT) {                                                                    \
-      case 4: launch_pfb_t<PL, 4>(x, n, h, M, y, tw, variant, fpg, st); break;       \
-      case 8: launch_pfb_t<PL, 8>(x, n, h, M, y, tw, variant, fpg, st); break;       \
-      case 16: launch_pfb_t<PL, 16>(x, n, h, M, y, tw, variant, fpg, st); break;     \
+      case 4: launch_pfb_t<PL, 4>(x, n, h, M, y, tw, st); break;                     \
+      case 8: launch_pfb_t<PL, 8>(x, n, h, M, y, tw, st); break;                     \
+      case 16: launch_pfb_t<PL, 16>(x, n, h, M, y, tw, st); break;                   \
       default: return hipErrorInvalidValue;                                          \
     }                                                                                \
     return hipGetLastError();                                                        \

@@ -6,14 +6,6 @@
 
 namespace vsig {
 
-// ---------------------------------------------------------------------------
-// Persistent-kernel skeleton shared by the streaming kernels: a block walks
-// units u = blockIdx.x, + gridDim.x, ...; the next unit's samples are loaded
-// into registers at the top of each iteration, so their HBM latency hides
-// behind the current unit's FFTs (the only global loads in flight are stream
-// loads: twiddles, window and filter spectra live in registers).
-// ---------------------------------------------------------------------------
-
 // spectrum: frames = (n - nperseg) / hop + 1; FPB frames per unit
 // (scipy.signal.spectrogram, scipy/signal/_spectral_py.py:2158-2205, as called
 // at utils.py:281-291).
@@ -30,184 +22,83 @@ __device__ __forceinline__ void psd_load(float2* v, const float2* __restrict__ x
   }
 }
 
-template <class P, int PERSIST>
-__global__ __launch_bounds__(block_threads<P>(), (min_waves<P, PERSIST>())) void psd_kernel(
+// Plans of >= 256 threads per frame (nfft >= 4096): two frames per block
+// through fft_pair (the LDS stores of one frame overlap the other's
+// butterflies), twiddles from register anchors.
+template <class P>
+__global__ __launch_bounds__(P::TF) void psd_pair_kernel(
+    const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
+    long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
+    const float2* __restrict__ tw) {
+  static_assert(P::TF >= 256, "one frame per block");
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  const long long u = blockIdx.x;
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 v[2][P::E];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    psd_load<P>(v[f], x, stride, nperseg, hop, u * 2 + f, nframes, t);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) {
+      const int i = in_index<P>(t, e);
+      const float w = i < nperseg ? win[i] : 0.f;
+      v[f][e] = make_float2(v[f][e].x * w, v[f][e].y * w);
+    }
+  }
+  launder_anchors<P>(wa);
+  fft_pair<P>(v[0], v[1], lds, TwAnchors{wa}, t);
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const long long frame = u * 2 + f;
+    if (frame < nframes) {
+      float* of = out + frame * P::N;
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = out_index<P>(t, e);
+        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+        __builtin_nontemporal_store((v[f][e].x * v[f][e].x + v[f][e].y * v[f][e].y) * scale, of + o);
+      }
+    }
+  }
+}
+
+// Smaller plans (several frames per 256-thread block): two-level twiddle
+// table in LDS and the real / imaginary parts exchanged in two rounds, so
+// four blocks fit a CU.
+template <class P>
+__global__ __launch_bounds__(block_threads<P>(), (P::E <= 16 ? 4 : 1)) void psd_split_kernel(
     const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
     const float2* __restrict__ tw) {
   constexpr int BT = block_threads<P>();
   constexpr int FPB = BT / P::TF;
-  __shared__ float2 lds[FPB * (PERSIST == 4 ? (P::LDS + 1) / 2 : P::LDS) +
-                       ((PERSIST == 3 || PERSIST == 4) ? tw2_size<P>() : 0)];
+  constexpr int FL = (P::LDS + 1) / 2;
+  __shared__ float2 lds[FPB * FL + tw2_size<P>()];
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
-  const long long units = (nframes + FPB - 1) / FPB;
-  long long u = PERSIST == 6 ? stage_bid<2>() : blockIdx.x;
-  if (u >= units) return;
-  if constexpr (PERSIST == 5 || PERSIST == 6) {   // register twiddle anchors; 6: two frames (fft_pair)
-    if constexpr (FPB != 1) return;                // launch_psd only picks these for TF >= 256
-    constexpr int NF = PERSIST == 6 ? 2 : 1;
-    float2 wa[nanch_total<P>()];
-    load_anchors<P>(wa, tw, t);
-    float2 v[NF][P::E];
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      psd_load<P>(v[f], x, stride, nperseg, hop, u * NF + f, nframes, t);
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = in_index<P>(t, e);
-        const float w = i < nperseg ? win[i] : 0.f;
-        v[f][e] = make_float2(v[f][e].x * w, v[f][e].y * w);
-      }
-    }
-    launder_anchors<P>(wa);
-    if constexpr (NF == 2) fft_pair<P>(v[0], v[1], lds, TwAnchors{wa}, t);
-    else fft_frame_anch<P>(v[0], lds, wa, t);
-#pragma unroll
-    for (int f = 0; f < NF; ++f) {
-      const long long frame = u * NF + f;
-      if (frame < nframes) {
-        float* of = out + frame * P::N;
-#pragma unroll
-        for (int e = 0; e < P::E; ++e) {
-          const int i = out_index<P>(t, e);
-          const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-          __builtin_nontemporal_store((v[f][e].x * v[f][e].x + v[f][e].y * v[f][e].y) * scale, of + o);
-        }
-      }
-    }
-    return;
-  }
-  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
-    constexpr int FL = (P::LDS + 1) / 2;
-    float2* t2 = lds + FPB * FL;
-    load_tw2<P>(t2, tw, threadIdx.x, BT);
-    float2 v[P::E];
-    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const int i = in_index<P>(t, e);
-      const float w = i < nperseg ? win[i] : 0.f;
-      v[e] = make_float2(v[e].x * w, v[e].y * w);
-    }
-    fft_frame_split<P>(v, reinterpret_cast<float*>(lds + fl * FL), t2, t);
-    const long long frame = u * FPB + fl;
-    if (frame < nframes) {
-      float* of = out + frame * P::N;
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = out_index<P>(t, e);
-        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
-      }
-    }
-    return;
-  }
-  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
-    float2* t2 = lds + FPB * P::LDS;
-    load_tw2<P>(t2, tw, threadIdx.x, BT);
-    float2 v[P::E];
-    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const int i = in_index<P>(t, e);
-      const float w = i < nperseg ? win[i] : 0.f;
-      v[e] = make_float2(v[e].x * w, v[e].y * w);
-    }
-    fft_frame_t2<P>(v, lds + fl * P::LDS, t2, t);
-    const long long frame = u * FPB + fl;
-    if (frame < nframes) {
-      float* of = out + frame * P::N;
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = out_index<P>(t, e);
-        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
-      }
-    }
-    return;
-  }
-
-  if constexpr (!PERSIST) {          // one unit per block, table twiddles
-    float2 v[P::E];
-    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const int i = in_index<P>(t, e);
-      const float w = i < nperseg ? win[i] : 0.f;
-      v[e] = make_float2(v[e].x * w, v[e].y * w);
-    }
-    fft_frame<P>(v, lds + fl * P::LDS, tw, t);
-    const long long frame = u * FPB + fl;
-    if (frame < nframes) {
-      float* of = out + frame * P::N;
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = out_index<P>(t, e);
-        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
-      }
-    }
-    return;
-  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
-    float2 v[P::E];
-    psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
-    for (; u < units; u += gridDim.x) {
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = in_index<P>(t, e);
-        const float w = i < nperseg ? win[i] : 0.f;
-        v[e] = make_float2(v[e].x * w, v[e].y * w);
-      }
-      float2 nv[P::E];
-      const long long nu = u + gridDim.x;
-      fft_frame_hook<P>(v, lds + fl * P::LDS, tw, t, [&] {
-        if (nu < units) psd_load<P>(nv, x, stride, nperseg, hop, nu * FPB + fl, nframes, t);
-      });
-      const long long frame = u * FPB + fl;
-      if (frame < nframes) {
-        float* of = out + frame * P::N;
-#pragma unroll
-        for (int e = 0; e < P::E; ++e) {
-          const int i = out_index<P>(t, e);
-          const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-          __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
-        }
-      }
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
-    }
-    return;
-  }
-  float2 wa[nanch_total<P>()];
-  load_anchors<P>(wa, tw, t);
-  float wr[P::E];
+  const long long u = blockIdx.x;
+  float2* t2 = lds + FPB * FL;
+  load_tw2<P>(t2, tw, threadIdx.x, BT);
+  float2 v[P::E];
+  psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const int i = in_index<P>(t, e);
-    wr[e] = i < nperseg ? win[i] : 0.f;
+    const float w = i < nperseg ? win[i] : 0.f;
+    v[e] = make_float2(v[e].x * w, v[e].y * w);
   }
-  float2 v[P::E];
-  psd_load<P>(v, x, stride, nperseg, hop, u * FPB + fl, nframes, t);
-  for (; u < units; u += gridDim.x) {
-    float2 nv[P::E];
-    const long long nu = u + gridDim.x;
-    if (nu < units) psd_load<P>(nv, x, stride, nperseg, hop, nu * FPB + fl, nframes, t);
+  fft_frame_split<P>(v, reinterpret_cast<float*>(lds + fl * FL), t2, t);
+  const long long frame = u * FPB + fl;
+  if (frame < nframes) {
+    float* of = out + frame * P::N;
 #pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = make_float2(v[e].x * wr[e], v[e].y * wr[e]);
-    fft_frame_anch<P>(v, lds + fl * P::LDS, wa, t);
-    const long long frame = u * FPB + fl;
-    if (frame < nframes) {
-      float* of = out + frame * P::N;
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = out_index<P>(t, e);
-        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
-      }
+    for (int e = 0; e < P::E; ++e) {
+      const int i = out_index<P>(t, e);
+      const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+      __builtin_nontemporal_store((v[e].x * v[e].x + v[e].y * v[e].y) * scale, of + o);
     }
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = nv[e];
   }
 }
 
@@ -239,6 +130,7 @@ __global__ __launch_bounds__(block_threads<P>()) void spectrum_prep(
   }
 }
 
+#ifdef VSIG_TUNING
 // ---------------------------------------------------------------------------
 // Engine micro-benchmark (tuning only): `iters` back-to-back FFTs of one frame
 // per block with no HBM traffic in the loop — the compute/LDS ceiling of a plan.
@@ -322,53 +214,31 @@ hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const fl
   }
   switch (key) {
     case -1024: VSIG_FB(Plan1024s) break;
-    case -2048: VSIG_FB(Plan2048s) break;
     case 4096: VSIG_FB(Plan4096) break;
     case 8192: VSIG_FB(Plan8192) break;
     case 16384: VSIG_FB(Plan16384) break;
-    case -16384: VSIG_FB(Plan16384w) break;
     default: return hipErrorInvalidValue;
   }
 #undef VSIG_FB
   return hipGetLastError();
 }
 
-// Grid cap of the persistent variants (0: every resident slot).  A cap of one
-// block per CU leaves the other slot to a concurrently launched correlator.
-static int g_psd_grid_cap = 0;
-void set_psd_grid_cap(int cap) { g_psd_grid_cap = cap; }
-
-template <class PL, int PERSIST>
-void launch_psd_t(const float2* x, long long stride, const float* win, int nperseg, long long hop,
-                  float scale, float* out, long long nframes, int shift, const float2* tw,
-                  hipStream_t st) {
-  constexpr int BT = block_threads<PL>();
-  constexpr int FPB = BT / PL::TF;
-  const long long units = (nframes + FPB - 1) / FPB;
-  long long grid =
-      (PERSIST == 1 || PERSIST == 2) ? persistent_grid(psd_kernel<PL, PERSIST>, BT, units)
-      : PERSIST == 6 ? (units + 1) / 2 : units;
-  if ((PERSIST == 1 || PERSIST == 2) && g_psd_grid_cap > 0 && grid > g_psd_grid_cap)
-    grid = g_psd_grid_cap;
-  hipLaunchKernelGGL((psd_kernel<PL, PERSIST>), dim3((unsigned)grid), dim3(BT), 0, st, x, stride,
-                     win, nperseg, hop, scale, out, nframes, shift, tw);
-}
+#endif  // VSIG_TUNING
 
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
                       long long hop, float scale, float* out, long long nframes, int shift,
-                      const float2* tw, int variant, hipStream_t st) {
+                      const float2* tw, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
   VSIG_PLAN_SWITCH(N, {
-    // bits 5/6 (anchors, frame pairs) need one frame per block (TF >= 256);
-    // smaller plans take the split-exchange kernel instead.
-    const bool big = PL::TF >= 256;
-    if ((variant & 64) && big) launch_psd_t<PL, 6>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
-    else if ((variant & 32) && big) launch_psd_t<PL, 5>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
-    else if (variant & (16 | 32 | 64)) launch_psd_t<PL, 4>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
-    else if (variant & 8) launch_psd_t<PL, 3>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
-    else if (variant & 4) launch_psd_t<PL, 2>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
-    else if (variant & 1) launch_psd_t<PL, 1>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
-    else launch_psd_t<PL, 0>(x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, st);
+    if constexpr (PL::TF >= 256) {
+      hipLaunchKernelGGL(psd_pair_kernel<PL>, dim3((unsigned)((nframes + 1) / 2)), dim3(PL::TF), 0,
+                         st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw);
+    } else {
+      constexpr int FPB = block_threads<PL>() / PL::TF;
+      hipLaunchKernelGGL(psd_split_kernel<PL>, dim3((unsigned)((nframes + FPB - 1) / FPB)),
+                         dim3(block_threads<PL>()), 0, st, x, stride, win, nperseg, hop, scale, out,
+                         nframes, shift, tw);
+    }
   });
   return hipGetLastError();
 }
@@ -392,29 +262,21 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 }
 
 hipError_t tw2_info(int N, int* shift, int* hi) {
-  if (N == -16384) { *shift = tw2_shift<Plan16384w>(); *hi = tw2_hi<Plan16384w>(); return hipSuccess; }
   if (N == -1024) { *shift = tw2_shift<Plan1024s>(); *hi = tw2_hi<Plan1024s>(); return hipSuccess; }
-  if (N == -2048) { *shift = tw2_shift<Plan2048s>(); *hi = tw2_hi<Plan2048s>(); return hipSuccess; }
   VSIG_PLAN_SWITCH(N, { *shift = tw2_shift<PL>(); *hi = tw2_hi<PL>(); });
   return hipSuccess;
 }
 
 hipError_t plan_info(int N, int* radices, int* npasses) {
-  if (N == -16384) {   // the E = 32 plan of 16384 points (variant bit 1)
-    *npasses = Plan16384w::NP;
-    for (int q = 0; q < Plan16384w::NP; ++q) radices[q] = Plan16384w::R[q];
-    return hipSuccess;
-  }
   if (N == -512 || N == -256) {     // decimating-FIR inverse plans
     const int np = N == -512 ? Plan512d::NP : Plan256d::NP;
     *npasses = np;
     for (int q = 0; q < np; ++q) radices[q] = N == -512 ? Plan512d::R[q] : Plan256d::R[q];
     return hipSuccess;
   }
-  if (N == -1024 || N == -2048) {   // one-wave overlap-save plans
-    const int np = N == -1024 ? Plan1024s::NP : Plan2048s::NP;
-    *npasses = np;
-    for (int q = 0; q < np; ++q) radices[q] = N == -1024 ? Plan1024s::R[q] : Plan2048s::R[q];
+  if (N == -1024) {                 // the one-wave overlap-save plan
+    *npasses = Plan1024s::NP;
+    for (int q = 0; q < Plan1024s::NP; ++q) radices[q] = Plan1024s::R[q];
     return hipSuccess;
   }
   VSIG_PLAN_SWITCH(N, {

@@ -175,6 +175,7 @@ hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* 
 
 }  // namespace vsig
 
+#ifdef VSIG_TUNING
 namespace vsig {
 // ---------------------------------------------------------------- copy probe
 // HBM ceiling probe for the tuning tools (tools/membw.py): copy n complex64
@@ -274,3 +275,4 @@ hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int varian
   return hipGetLastError();
 }
 }  // namespace vsig
+#endif  // VSIG_TUNING

@@ -27,14 +27,17 @@ struct vsig_ctx {
   PeakPartial* result = nullptr;         // scratch device result
   void* stage[3] = {nullptr, nullptr, nullptr};  // host-API device staging
   size_t stage_bytes[3] = {0, 0, 0};
+  void* conv[3] = {nullptr, nullptr, nullptr};   // complex128 path: c64 operands / output
+  size_t conv_bytes[3] = {0, 0, 0};
+  void* rscratch = nullptr;              // refine.hip scratch (keys first)
+  size_t rscratch_bytes = 0;
+  int refine = 1;                        // exact re-rank of the correlators' peak
+  int refine_eps_ppm = 1000;             // fp32 candidate band (relative, ppm of max |c|)
+  long long refine_cap = 1LL << 20;      // max outputs revisited (else record left fp32)
+  bool refine_ran = false;
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
-  vsig::Variants var{64, 320, 193};       // tuned defaults (see vsig_set_option)
-  int fir_m = 0, xcorr_m = 0;            // 0: size rule; else forced block size
-  int pfb_variant = 3, pfb_fpg = 64;
-  int psd_grid = 0;                     // persistent PSD: grid cap (0 = all resident slots)
-  int fir_psd_variant = 0;              // bit 0: non-temporal filtered-stream stores     // PFB: LDS-staged stores + row prefetch; frames per group
 };
 
 struct vsig_fir {
@@ -44,11 +47,18 @@ struct vsig_fir {
   float2* Hs;
 };
 
+// A correlation template: L <= 8192 one spectrum of M points; longer
+// templates a spectrum per 8192-sample chunk (M = 16384), applied as a sum of
+// passes accumulated in c (a scratch kept with the handle when the caller
+// passes none).  tmpl: the template on the device (refine pass).
 struct vsig_xcorr {
   vsig_ctx* ctx;
-  int L, M;
-  float2* Ps;
-  float2* Ps1;   // partitioned mode: spectrum of the template's second half (else null)
+  long long L;
+  int M;
+  std::vector<float2*> Ps;
+  float2* tmpl = nullptr;
+  void* cbuf = nullptr;
+  size_t cbuf_bytes = 0;
 };
 
 namespace {
@@ -94,12 +104,6 @@ int get_twiddles(vsig_ctx* c, int N, const float2** out) {
   return VSIG_OK;
 }
 
-// Twiddle-table key of the plan an overlap-save launch of size M uses.
-int tw_key(int M, int variant) {
-  if (M == 1024 || M == 2048) return -M;           // one-wave plans
-  return (M == 16384 && (variant & 2)) ? -16384 : M;
-}
-
 // Two-level table for plan key N (cached under key N + 2^20).
 int get_tw2(vsig_ctx* c, int N, const float2** out) {
   const int key = N + (1 << 20);
@@ -124,13 +128,6 @@ int get_tw2(vsig_ctx* c, int N, const float2** out) {
   c->tw[key] = d;
   *out = d;
   return VSIG_OK;
-}
-
-// Twiddle operand of a launch: the per-pass table, or (variant bits 3/4) the
-// two-level table.  os: an overlap-save launch (its own plans for 1k / 2k / 16k).
-int get_tw_for(vsig_ctx* c, int M, int variant, bool os, const float2** out) {
-  const int key = os ? tw_key(M, variant) : M;
-  return (variant & 24) ? get_tw2(c, key, out) : get_twiddles(c, key, out);   // anchors: per-pass table
 }
 
 // W_M^t for t < T (the per-thread twiddle of the half-frame correlator),
@@ -195,38 +192,29 @@ bool pow2_in(long long v, long long lo, long long hi) {
   return v >= lo && v <= hi && (v & (v - 1)) == 0;
 }
 
-// VSIG_FIR_M / VSIG_XCORR_M: tuning overrides of the overlap-save block size.
-int env_size(const char* name, int dflt, int minlen) {
-  const char* e = getenv(name);
-  if (!e) return dflt;
-  const int v = atoi(e);
-  if ((v == 1024 || v == 2048 || v == 4096 || v == 8192 || v == 16384) && v >= 2 * minlen)
-    return v;
-  return dflt;
-}
-
-int os_size_fir_default(int ntaps) {
+// Overlap-save block sizes (measured best on MI355X for the chain's sizes).
+int os_size_fir(int ntaps) {
   if (ntaps <= 256) return 1024;      // one-wave blocks; hop >= 769 (measured best at 255 taps)
   if (ntaps <= 512) return 4096;
   if (ntaps <= 2048) return 8192;
   if (ntaps <= 8192) return 16384;
   return 0;
 }
-int os_size_fir(const vsig_ctx* c, int ntaps) {
-  int d = os_size_fir_default(ntaps);
-  if (d && c->fir_m >= 2 * ntaps) d = c->fir_m;
-  return d ? env_size("VSIG_FIR_M", d, ntaps) : 0;
-}
-int os_size_xcorr_default(int L) {
+int os_size_xcorr(long long L) {
   if (L <= 1024) return 4096;
   if (L <= 2048) return 8192;
   if (L <= 8192) return 16384;
   return 0;
 }
-int os_size_xcorr(const vsig_ctx* c, int L) {
-  int d = os_size_xcorr_default(L);
-  if (d && c->xcorr_m >= 2 * L) d = c->xcorr_m;
-  return d ? env_size("VSIG_XCORR_M", d, L) : 0;
+
+int ensure_buf(vsig_ctx* c, void** buf, size_t* have, size_t bytes) {
+  if (bytes <= *have) return VSIG_OK;
+  if (*buf) (void)hipFree(*buf);
+  *buf = nullptr;
+  *have = 0;
+  HIPCHK(c, hipMalloc(buf, bytes));
+  *have = bytes;
+  return VSIG_OK;
 }
 
 // FFT_M(zero-padded u[0..len)) * gain into a new device buffer.
@@ -249,45 +237,58 @@ int finalize_peak(vsig_ctx* c, long long nparts, int sqrt_max, vsig_peak_t* peak
   return VSIG_OK;
 }
 
-// Shared by the plan-based and the general correlation paths.  Ps1 != null:
-// partitioned correlation (template halves of M/2, see xcorr_part_kernel).
-int run_xcorr(vsig_ctx* c, int M, const float2* Ps, const float2* Ps1, int L, const float2* s,
-              long long n, long long off, long long nout, int store_mode, void* cout,
-              vsig_peak_t* peak_dev) {
-  if (nout <= 0) return fail(c, VSIG_E_INVALID, "empty correlation output");
-  const long long hop = Ps1 ? (long long)M / 2 : (long long)M - L + 1;
-  const long long nblocks = (nout + hop - 1) / hop;
-  const int var = Ps1 ? (c->var.xcorr & 8) : c->var.xcorr;
-  const long long nparts = nblocks * vsig::os_waves(M, var);   // one partial per wave
-  int rc = ensure_partials(c, nparts);
-  if (rc) return rc;
-  const float2* tw;
-  const float2* wt = nullptr;
-  if (!Ps1 && M == 16384 && (var & 64)) {    // half-frame correlator: 8192-point plan
-    rc = (var & 8) ? get_tw2(c, 8192, &tw) : get_twiddles(c, 8192, &tw);
-    if (rc) return rc;
-    rc = get_half_tw(c, M, 256, &wt);
+// Operands of the refine pass: np.correlate(a, v) in the final output
+// space (o <-> full index F + o), complex128 or complex64 on the device.
+struct RefineOperands {
+  const void* a; long long na;
+  const void* v; long long nv;
+  int c128;
+  long long F;
+};
+
+// Re-rank the peak record rec (finalized, max |c|) over the outputs within the
+// fp32 band; src: the correlator's wave partials (geometry of an M-point
+// launch with raw->final reversal rev) or, if c64 != null, a stored c64 array.
+int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, long long hop,
+               long long nparts, int rev, const float2* c64, PeakPartial* rec, void* out128) {
+  c->refine_ran = false;
+  if (!c->refine) return VSIG_OK;
+  vsig::RefineArgs r{};
+  r.a = op.a; r.na = op.na; r.v = op.v; r.nv = op.nv; r.c128 = op.c128;
+  r.nout = nout; r.F = op.F; r.rev = rev;
+  if (c64) {
+    r.from_array = 1; r.c64 = c64; r.Q = 1; r.stride = 0; r.waves = 1; r.hop = 64;
   } else {
-    rc = get_tw_for(c, M, var, true, &tw);
+    int waves, Q, stride, plan;
+    if (vsig::xcorr_geom(M, &waves, &Q, &stride, &plan) != hipSuccess)
+      return fail(c, VSIG_E_INVALID, "refine: no correlator geometry for M");
+    r.parts = c->partials; r.nparts = nparts; r.hop = hop;
+    r.waves = waves; r.Q = Q; r.stride = stride;
   }
+  r.eps = c->refine_eps_ppm * 1e-6;
+  r.eps2 = 1e-6;
+  r.cap_items = c->refine_cap / (64LL * r.Q);
+  if (r.cap_items < 1) r.cap_items = 1;
+  int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, vsig::refine_scratch_bytes(r.cap_items, r.Q));
   if (rc) return rc;
-  {
-    Timed t(c, "xcorr");
-    if (Ps1)
-      HIPCHK(c, vsig::launch_xcorr_part(M, s, n, Ps, Ps1, off, nout, (float2*)cout, store_mode,
-                                        c->partials, tw, (var & 8) ? 1 : 0, c->stream));
-    else
-      HIPCHK(c, vsig::launch_xcorr_os(M, s, n, Ps, off, nout, hop, (float2*)cout, store_mode,
-                                      c->partials, tw, wt, c->var.xcorr, c->stream));
-  }
-  return finalize_peak(c, nparts, 1, peak_dev);
+  r.scratch = c->rscratch;
+  r.rec = rec;
+  r.out128 = out128;
+  Timed t(c, "refine");
+  HIPCHK(c, vsig::launch_refine(r, c->stream));
+  c->refine_ran = true;
+  return VSIG_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
-int vsig_version(void) { return 1; }
+#ifndef VSIG_SRC_HASH
+#define VSIG_SRC_HASH "unknown"
+#endif
+int vsig_version(void) { return 2; }
+const char* vsig_build_id(void) { return VSIG_SRC_HASH; }
 
 const char* vsig_errstr(int s) {
   switch (s) {
@@ -312,9 +313,6 @@ int vsig_init(int device, vsig_ctx** out) {
   c->device = device;
   if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) { delete c; return VSIG_E_HIP; }
   c->stream = c->own;
-  if (const char* e = getenv("VSIG_PSD_VARIANT")) c->var.psd = atoi(e);
-  if (const char* e = getenv("VSIG_FIR_VARIANT")) c->var.fir = atoi(e);
-  if (const char* e = getenv("VSIG_XCORR_VARIANT")) c->var.xcorr = atoi(e);
   if (hipMalloc(&c->result, sizeof(PeakPartial)) != hipSuccess) { vsig_free(c); return VSIG_E_NOMEM; }
   *out = c;
   return VSIG_OK;
@@ -337,6 +335,8 @@ void vsig_free(vsig_ctx* c) {
   if (c->partials) (void)hipFree(c->partials);
   if (c->result) (void)hipFree(c->result);
   for (int i = 0; i < 3; ++i) if (c->stage[i]) (void)hipFree(c->stage[i]);
+  for (int i = 0; i < 3; ++i) if (c->conv[i]) (void)hipFree(c->conv[i]);
+  if (c->rscratch) (void)hipFree(c->rscratch);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -352,25 +352,14 @@ int vsig_set_stream(vsig_ctx* c, void* s) {
 int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   if (!c || !key) return VSIG_E_INVALID;
   const std::string k(key);
-  if (k == "psd_variant") c->var.psd = value & 125;
-  else if (k == "fir_variant") c->var.fir = value & 511;
-  else if (k == "xcorr_variant") c->var.xcorr = value & 255;
-  else if (k == "fir_m" || k == "xcorr_m") {
-    if (value != 0 && value != 1024 && value != 2048 && value != 4096 && value != 8192 &&
-        value != 16384)
-      return fail(c, VSIG_E_INVALID, "block size must be 0, 1024, 2048, 4096, 8192 or 16384");
-    (k == "fir_m" ? c->fir_m : c->xcorr_m) = value;
-  } else if (k == "pfb_variant") {
-    c->pfb_variant = value & 7;
-  } else if (k == "psd_grid") {
-    if (value < 0) return fail(c, VSIG_E_INVALID, "psd_grid must be >= 0");
-    c->psd_grid = value;
-    vsig::set_psd_grid_cap(value);
-  } else if (k == "fir_psd_variant") {
-    c->fir_psd_variant = value & 7;
-  } else if (k == "pfb_fpg") {
-    if (value < 0 || value > 65536) return fail(c, VSIG_E_INVALID, "pfb_fpg must be in [0, 65536]");
-    c->pfb_fpg = value;
+  if (k == "refine") {
+    c->refine = value != 0;
+  } else if (k == "refine_eps_ppm") {
+    if (value < 1 || value > 500000) return fail(c, VSIG_E_INVALID, "refine_eps_ppm must be in [1, 500000]");
+    c->refine_eps_ppm = value;
+  } else if (k == "refine_cap") {
+    if (value < 4096) return fail(c, VSIG_E_INVALID, "refine_cap must be >= 4096");
+    c->refine_cap = value;
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }
@@ -380,19 +369,27 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
 int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
   if (!c || !key || !value) return VSIG_E_INVALID;
   const std::string k(key);
-  if (k == "psd_variant") *value = c->var.psd;
-  else if (k == "fir_variant") *value = c->var.fir;
-  else if (k == "xcorr_variant") *value = c->var.xcorr;
-  else if (k == "fir_m") *value = c->fir_m;
-  else if (k == "xcorr_m") *value = c->xcorr_m;
-  else if (k == "pfb_variant") *value = c->pfb_variant;
-  else if (k == "pfb_fpg") *value = c->pfb_fpg;
-  else if (k == "fir_psd_variant") *value = c->fir_psd_variant;
-  else if (k == "psd_grid") *value = c->psd_grid;
+  if (k == "refine") *value = c->refine;
+  else if (k == "refine_eps_ppm") *value = c->refine_eps_ppm;
+  else if (k == "refine_cap") *value = (int)c->refine_cap;
   else return VSIG_E_INVALID;
   return VSIG_OK;
 }
 
+int vsig_refine_status(vsig_ctx* c, int32_t* status, int64_t* candidates) {
+  if (!c || !status || !candidates) return VSIG_E_INVALID;
+  *status = 2;
+  *candidates = 0;
+  if (!c->refine_ran || !c->rscratch) return VSIG_OK;
+  unsigned long long keys[5];
+  HIPCHK(c, hipMemcpyAsync(keys, c->rscratch, sizeof(keys), hipMemcpyDeviceToHost, c->stream));
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  *status = keys[4] ? 1 : 0;
+  *candidates = (int64_t)keys[0];
+  return VSIG_OK;
+}
+
+#ifdef VSIG_TUNING
 int vsig_fft_bench(vsig_ctx* c, int key, void* io, int frames, int iters, int twl) {
   if (!c || !io || frames < 1 || iters < 1) return fail(c, VSIG_E_INVALID, "bad arguments");
   const float2* tw;
@@ -409,6 +406,7 @@ int vsig_copy_bench(vsig_ctx* c, const void* x, int64_t n, void* y, int variant,
   HIPCHK(c, vsig::launch_copy_probe((const float2*)x, n, (float2*)y, variant, grid, c->stream));
   return VSIG_OK;
 }
+#endif
 
 int vsig_synchronize(vsig_ctx* c) {
   if (!c) return VSIG_E_INVALID;
@@ -450,16 +448,13 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
     return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
   const float2* tw;
-  // anchor / pair variants (bits 5, 6) read the per-pass table and run for
-  // plans of >= 256 threads per frame; below that they fall back to the
-  // split-exchange kernel and its two-level table (see launch_psd)
-  const int pv = c->var.psd;
-  const bool anch = (pv & 96) && vsig::psd_plan_threads(nfft) >= 256;
-  int rc = (!anch && (pv & (8 | 16 | 32 | 64))) ? get_tw2(c, nfft, &tw) : get_twiddles(c, nfft, &tw);
+  // pair kernel (>= 256 threads per frame): per-pass table; smaller plans: two-level table
+  const bool pair = vsig::psd_plan_threads(nfft) >= 256;
+  int rc = pair ? get_twiddles(c, nfft, &tw) : get_tw2(c, nfft, &tw);
   if (rc) return rc;
   Timed t(c, "psd");
   HIPCHK(c, vsig::launch_psd(nfft, (const float2*)x, stride, win, nperseg, hop, scale, sxx, nframes,
-                             shift, tw, c->var.psd, c->stream));
+                             shift, tw, c->stream));
   return VSIG_OK;
 }
 
@@ -487,7 +482,7 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
   if (!c || !taps || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   *out = nullptr;
   if (ntaps < 1 || decim < 1) return fail(c, VSIG_E_INVALID, "ntaps and decim must be >= 1");
-  const int M = os_size_fir(c, ntaps);
+  const int M = os_size_fir(ntaps);
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "ntaps > 8192");
   long long hop = ((long long)M - (ntaps - 1)) / decim * decim;
   if (hop < 1) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
@@ -520,7 +515,7 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
   int rc;
-  if ((c->var.fir & 256) && f->M == 1024 && (f->decim == 2 || f->decim == 4)) {
+  if (f->M == 1024 && (f->decim == 2 || f->decim == 4)) {
     // decimation in the frequency domain: M/D-point inverse transforms
     const float2* twd;
     if ((rc = get_twiddles(c, -1024, &tw)) || (rc = get_twiddles(c, -1024 / f->decim, &twd))) return rc;
@@ -533,39 +528,17 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
                                    tw, twd, c->stream, mix));
     return VSIG_OK;
   }
-  if (mix && ((c->var.fir & (8 | 16 | 128)) || !(c->var.fir & 64) || f->M != 1024))
-    return fail(c, VSIG_E_UNSUPPORTED, "fused mixer needs the default FIR variant and ntaps <= 256");
-  rc = get_tw_for(c, f->M, c->var.fir, true, &tw);
+  if (mix && f->M != 1024)
+    return fail(c, VSIG_E_UNSUPPORTED, "fused mixer needs the 1024-point block (ntaps <= 256)");
+  rc = get_twiddles(c, f->M == 1024 ? -1024 : f->M, &tw);
   if (rc) return rc;
   Timed t(c, "fir");
   HIPCHK(c, vsig::launch_fir_os(f->M, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps, f->hop,
-                                f->decim, (float2*)y, tw, c->var.fir, c->stream, mix));
+                                f->decim, (float2*)y, tw, c->stream, mix));
   return VSIG_OK;
 }
 
 int vsig_fir_block(const vsig_fir* f) { return f ? f->M : 0; }
-
-int vsig_fir_psd_exec_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y,
-                          int64_t ny, const float* win, int32_t nfft, float scale, int32_t shift,
-                          float* sxx, int64_t nframes) {
-  if (!f) return VSIG_E_INVALID;
-  vsig_ctx* c = f->ctx;
-  if (!x || !y || !win || (!sxx && nframes > 0)) return fail(c, VSIG_E_INVALID, "null pointer");
-  if (n < 1 || nhist < 0) return fail(c, VSIG_E_INVALID, "need n >= 1 and nhist >= 0");
-  if (ny != n) return fail(c, VSIG_E_INVALID, "ny != n");
-  if (f->decim != 1 || f->M != 1024 || vsig::fir_psd_seg_hop(nfft) == 0 ||
-      f->ntaps - 1 + vsig::fir_psd_seg_hop(nfft) > 1024)
-    return fail(c, VSIG_E_UNSUPPORTED, "fused filter+spectrum: decim 1, nfft 8192, ntaps <= 342");
-  if (nframes != ny / nfft) return fail(c, VSIG_E_INVALID, "nframes != ny / nfft");
-  const float2 *twf, *tws;
-  int rc;
-  if ((rc = get_twiddles(c, -1024, &twf)) || (rc = get_twiddles(c, nfft, &tws))) return rc;
-  Timed t(c, "fir_psd");
-  HIPCHK(c, vsig::launch_fir_psd(nfft, (const float2*)x, nhist + n, nhist, f->Hs, f->ntaps,
-                                 (float2*)y, win, scale, shift, sxx, nframes, twf, tws,
-                                 c->fir_psd_variant, c->stream));
-  return VSIG_OK;
-}
 
 int vsig_fir_exec_hist_dev(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* y,
                            int64_t ny) {
@@ -619,43 +592,124 @@ int vsig_fir_c64(vsig_ctx* c, const void* x, int64_t n, const float* taps, int32
 }
 
 // ---------------------------------------------------------------- correlation
-int vsig_xcorr_create(vsig_ctx* c, const void* tmpl, int32_t L, vsig_xcorr** out) {
+// Template spectra from a device c64 template of L samples: L <= 8192 one
+// M-point spectrum; longer templates one M = 16384 spectrum per 8192-sample
+// chunk (sum of passes, see xcorr_run).
+static int xcorr_build(vsig_ctx* c, const float2* td, long long L, vsig_xcorr* x) {
+  constexpr long long B = 8192;
+  x->ctx = c;
+  x->L = L;
+  x->M = L <= B ? os_size_xcorr(L) : 16384;
+  for (long long p = 0; p * B < L || p == 0; ++p) {
+    const long long Lp = L <= B ? L : ((L - p * B) < B ? (L - p * B) : B);
+    float2* P = nullptr;
+    const int rc = make_spectrum(c, td + p * B, (int)Lp, x->M, &P);
+    if (rc) return rc;
+    x->Ps.push_back(P);
+    if (L <= B) break;
+  }
+  return VSIG_OK;
+}
+
+static void xcorr_release(vsig_xcorr* x) {
+  (void)hipStreamSynchronize(x->ctx->stream);
+  for (float2* P : x->Ps) (void)hipFree(P);
+  x->Ps.clear();
+  if (x->tmpl) (void)hipFree(x->tmpl);
+  if (x->cbuf) (void)hipFree(x->cbuf);
+  x->tmpl = nullptr;
+  x->cbuf = nullptr;
+}
+
+// The correlation c[o] = sum_k s[o - off + k] conj(p[k]) of the handle's
+// template over the c64 stream s, o < nout, stored per store_mode bits 0-2
+// into cout (c64, may be null), the peak record into rec, then refined with
+// op (see run_refine; out128: complex128 c to patch).  Templates longer than
+// 8192: the chunks' passes accumulate in c (store bit 8; a scratch kept with
+// the handle when cout is null), then one fp64 peak reduction over c and the
+// refine from the stored array.
+static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off, long long nout,
+                     int store_mode, float2* cout, vsig_peak_t* peak_dev,
+                     const RefineOperands* op, void* out128) {
+  vsig_ctx* c = x->ctx;
+  PeakPartial* rec = peak_dev ? reinterpret_cast<PeakPartial*>(peak_dev) : c->result;
+  if (x->Ps.size() == 1 && x->L <= 8192) {
+    const long long hop = (long long)x->M - x->L + 1;
+    const long long nblocks = (nout + hop - 1) / hop;
+    int waves, Q, stride, plan;
+    if (vsig::xcorr_geom(x->M, &waves, &Q, &stride, &plan) != hipSuccess)
+      return fail(c, VSIG_E_UNSUPPORTED, "correlator block size");
+    const long long nparts = nblocks * waves;   // one partial per wave
+    int rc = ensure_partials(c, nparts);
+    if (rc) return rc;
+    const float2* tw;
+    const float2* wt = nullptr;
+    if ((rc = get_twiddles(c, plan, &tw))) return rc;
+    if (x->M == 16384 && (rc = get_half_tw(c, x->M, 256, &wt))) return rc;
+    {
+      Timed t(c, "xcorr");
+      HIPCHK(c, vsig::launch_xcorr_os(x->M, s, n, x->Ps[0], off, nout, hop, cout, store_mode,
+                                      c->partials, tw, wt, c->stream));
+    }
+    if ((rc = finalize_peak(c, nparts, 1, peak_dev))) return rc;
+    if (!op) return VSIG_OK;
+    if (out128 && cout) HIPCHK(c, vsig::launch_convert_c(1, cout, nout, out128, c->stream));
+    return run_refine(c, *op, nout, x->M, hop, nparts, (store_mode & 4) ? 1 : 0, nullptr, rec, out128);
+  }
+  constexpr long long B = 8192;
+  constexpr int M = 16384;
+  float2* cbuf = cout;
+  int rc;
+  if (!cbuf) {
+    if ((rc = ensure_buf(c, &x->cbuf, &x->cbuf_bytes, (size_t)nout * sizeof(float2)))) return rc;
+    cbuf = static_cast<float2*>(x->cbuf);
+  }
+  const float2 *tw, *wt;
+  if ((rc = get_twiddles(c, 8192, &tw)) || (rc = get_half_tw(c, M, 256, &wt))) return rc;
+  {
+    Timed t(c, "xcorr");            // the whole chunked correlation + its peak pass
+    for (size_t p = 0; p < x->Ps.size(); ++p) {
+      const long long Lp = (x->L - (long long)p * B) < B ? (x->L - (long long)p * B) : B;
+      const int mode = (store_mode & 4 ? 2 | 4 : 1) | (p ? 8 : 0);
+      HIPCHK(c, vsig::launch_xcorr_os(M, s, n, x->Ps[p], off - (long long)p * B, nout,
+                                      (long long)M - Lp + 1, cbuf, mode, nullptr, tw, wt,
+                                      c->stream));
+    }
+    if ((rc = vsig_peak_dev(c, VSIG_DTYPE_C64, cbuf, nout, peak_dev))) return rc;
+  }
+  if (!op) return VSIG_OK;
+  if (out128 && cout) HIPCHK(c, vsig::launch_convert_c(1, cout, nout, out128, c->stream));
+  return run_refine(c, *op, nout, M, 0, 0, 0, cbuf, rec, out128);
+}
+
+int vsig_xcorr_create(vsig_ctx* c, const void* tmpl, int64_t L, vsig_xcorr** out) {
   if (!c || !tmpl || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   *out = nullptr;
   if (L < 1) return fail(c, VSIG_E_INVALID, "template length must be >= 1");
-  // Partitioned mode (variant bit 5): M = next power of two >= L, halves of M/2.
-  int Mp = 2048;
-  while (Mp < L) Mp *= 2;
-  const bool part = (c->var.xcorr & 32) && L > 1024 && Mp <= 16384;
-  const int M = part ? Mp : os_size_xcorr(c, L);
-  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "template longer than 8192");
-  float2* td = nullptr;
-  HIPCHK(c, hipMalloc(&td, (size_t)L * sizeof(float2)));
-  hipError_t e = hipMemcpyAsync(td, tmpl, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, c->stream);
-  if (e != hipSuccess) { (void)hipFree(td); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
-  float2 *Ps = nullptr, *Ps1 = nullptr;
-  int rc;
-  if (part) {
-    rc = make_spectrum(c, td, M / 2, M, &Ps);
-    if (!rc) rc = make_spectrum(c, td + M / 2, L - M / 2, M, &Ps1);
-  } else {
-    rc = make_spectrum(c, td, L, M, &Ps);
+  vsig_xcorr* x = new vsig_xcorr();
+  x->ctx = c;
+  hipError_t e = hipMalloc(&x->tmpl, (size_t)L * sizeof(float2));
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(x->tmpl, tmpl, (size_t)L * sizeof(float2), hipMemcpyHostToDevice, c->stream);
+  if (e != hipSuccess) {
+    xcorr_release(x);
+    delete x;
+    return fail(c, e == hipErrorOutOfMemory ? VSIG_E_NOMEM : VSIG_E_HIP, hipGetErrorString(e));
   }
+  const int rc = xcorr_build(c, x->tmpl, L, x);
   (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(td);
   if (rc) {
-    if (Ps) (void)hipFree(Ps);
+    xcorr_release(x);
+    delete x;
     return rc;
   }
-  *out = new vsig_xcorr{c, L, M, Ps, Ps1};
+  *out = x;
   return VSIG_OK;
 }
 
 void vsig_xcorr_free(vsig_xcorr* x) {
   if (!x) return;
-  (void)hipStreamSynchronize(x->ctx->stream);
-  (void)hipFree(x->Ps);
-  if (x->Ps1) (void)hipFree(x->Ps1);
+  xcorr_release(x);
   delete x;
 }
 
@@ -669,55 +723,17 @@ int vsig_xcorr_exec_dev(vsig_xcorr* x, const void* s, int64_t n, int32_t mode, v
   else if (mode == VSIG_MODE_FULL) { off = x->L - 1; nout = n + x->L - 1; }
   else return fail(c, VSIG_E_INVALID, "streaming correlation supports VALID and FULL");
   if (nout < 1) return fail(c, VSIG_E_INVALID, "stream shorter than the template");
-  return run_xcorr(c, x->M, x->Ps, x->Ps1, x->L, (const float2*)s, n, off, nout, cout ? 1 : 0,
-                   cout, peak_dev);
+  // np.correlate(s, p): output o is full index (L - 1 - off) + o
+  const RefineOperands op{s, n, x->tmpl, x->L, 0, (x->L - 1) - off};
+  return xcorr_run(x, (const float2*)s, n, off, nout, cout ? 1 : 0, (float2*)cout, peak_dev, &op,
+                   nullptr);
 }
 
-// Templates longer than 8192 (np.correlate has no length limit): the
-// template is cut into chunks of B = 8192 samples and the correlation is the
-// sum of the chunks' correlations, chunk p shifted by p B (kernel offset
-// off - p B, same output range); each chunk runs the M = 16384 correlator and
-// adds into c (store bit 8), then one peak reduction over the summed c
-// (first maximum, fp64 sums) gives find_correlation_peak's record.  Costs
-// ceil(L / 8192) passes over the stream plus the read-modify-write of c.
-static int correlate_chunked(vsig_ctx* c, const float2* tmpl, long long L, const float2* strm,
-                             long long n, long long off, long long nout, bool swap, float2* cout,
-                             vsig_peak_t* peak_dev) {
-  constexpr int B = 8192, M = 16384;
-  float2* cbuf = cout;
-  if (!cbuf) HIPCHK(c, hipMalloc(&cbuf, (size_t)nout * sizeof(float2)));
-  const float2 *tw, *wt;
-  int rc = 0;
-  const int var = (c->var.xcorr & 64) ? c->var.xcorr : 193;   // the half-frame kernel
-  if ((rc = (var & 8) ? get_tw2(c, 8192, &tw) : get_twiddles(c, 8192, &tw)) ||
-      (rc = get_half_tw(c, M, 256, &wt))) {
-    if (!cout) (void)hipFree(cbuf);
-    return rc;
-  }
-  for (long long p = 0; p * B < L && !rc; ++p) {
-    const int Lp = (int)((L - p * B) < B ? (L - p * B) : B);
-    float2* Ps = nullptr;
-    if ((rc = make_spectrum(c, tmpl + p * B, Lp, M, &Ps))) break;
-    const int mode = (swap ? 2 | 4 : 1) | (p ? 8 : 0);
-    {
-      Timed t(c, "xcorr");
-      hipError_t e = vsig::launch_xcorr_os(M, strm, n, Ps, off - p * B, nout, (long long)M - Lp + 1,
-                                           cbuf, mode, nullptr, tw, wt, var, c->stream);
-      if (e != hipSuccess) rc = fail(c, VSIG_E_HIP, hipGetErrorString(e));
-    }
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(Ps);
-  }
-  if (!rc) rc = vsig_peak_dev(c, VSIG_DTYPE_C64, cbuf, nout, peak_dev);   // null: c->result
-  if (!cout) {
-    (void)hipStreamSynchronize(c->stream);
-    (void)hipFree(cbuf);
-  }
-  return rc;
-}
-
-int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
-                           int32_t mode, void* cout, vsig_peak_t* peak_dev) {
+// np.correlate(a, v, mode): the shorter operand is the template; with
+// nv > na the correlation of v by a is computed and stored conj() reversed.
+static int correlate_impl(vsig_ctx* c, int in128, const void* a, long long na, const void* v,
+                          long long nv, int32_t mode, int out128, void* cout,
+                          vsig_peak_t* peak_dev) {
   if (!c || !a || !v) return fail(c, VSIG_E_INVALID, "null pointer");
   if (na < 1 || nv < 1) return fail(c, VSIG_E_INVALID, "empty input");  // numeric.py:865-868
   const long long nmin = na < nv ? na : nv, nmax = na < nv ? nv : na;
@@ -726,49 +742,86 @@ int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v
   else if (mode == VSIG_MODE_VALID) { F = nmin - 1; nout = nmax - nmin + 1; }
   else if (mode == VSIG_MODE_SAME) { F = na >= nv ? nmin - 1 - nmin / 2 : nmin / 2; nout = nmax; }
   else return fail(c, VSIG_E_INVALID, "mode must be VALID, FULL or SAME");
+  int rc;
+  // complex64 operands of the FFT pass (complex128 callers: converted copies)
+  const float2 *a64 = (const float2*)a, *v64 = (const float2*)v;
+  if (in128) {
+    if ((rc = ensure_buf(c, &c->conv[0], &c->conv_bytes[0], (size_t)na * 8)) ||
+        (rc = ensure_buf(c, &c->conv[1], &c->conv_bytes[1], (size_t)nv * 8)))
+      return rc;
+    HIPCHK(c, vsig::launch_convert_c(0, a, na, c->conv[0], c->stream));
+    HIPCHK(c, vsig::launch_convert_c(0, v, nv, c->conv[1], c->stream));
+    a64 = (const float2*)c->conv[0];
+    v64 = (const float2*)c->conv[1];
+  }
+  float2* c64 = (float2*)cout;
+  if (out128 && cout) {
+    if ((rc = ensure_buf(c, &c->conv[2], &c->conv_bytes[2], (size_t)nout * 8))) return rc;
+    c64 = (float2*)c->conv[2];
+  }
   const bool swap = nv > na;  // template must be the shorter operand
-  const float2* tmpl = (const float2*)(swap ? a : v);
-  const float2* strm = (const float2*)(swap ? v : a);
+  const float2* tmpl = swap ? a64 : v64;
+  const float2* strm = swap ? v64 : a64;
   // c[o] = full[F + o]; full[i] = sum_k a[i-(nv-1)+k] conj(v[k]).
   // Not swapped: kernel offset off = (L-1) - F.  Swapped: compute the
   // correlation of v by a and store conj() reversed, off' = F + nout - nv.
   const long long off = swap ? F + nout - nv : (nmin - 1) - F;
-  if (nmin > 8192) return correlate_chunked(c, tmpl, nmin, strm, nmax, off, nout, swap,
-                                            (float2*)cout, peak_dev);
-  const int L = (int)nmin;
-  const int M = os_size_xcorr(c, L);
-  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "shorter operand longer than 8192");
-  float2* Ps = nullptr;
-  int rc = make_spectrum(c, tmpl, L, M, &Ps);
-  if (rc) return rc;
-  rc = run_xcorr(c, M, Ps, nullptr, L, strm, nmax, off, nout,
-                 (cout ? (swap ? 2 : 1) : 0) | (swap ? 4 : 0), cout,
-                 peak_dev);
-  (void)hipStreamSynchronize(c->stream);
-  (void)hipFree(Ps);
+  vsig_xcorr x;
+  x.ctx = c;
+  rc = xcorr_build(c, tmpl, nmin, &x);
+  if (!rc) {
+    const RefineOperands op{a, na, v, nv, in128, F};
+    const int store = (cout ? (swap ? 2 : 1) : 0) | (swap ? 4 : 0);
+    rc = xcorr_run(&x, strm, nmax, off, nout, store, c64, peak_dev, &op, out128 ? cout : nullptr);
+  }
+  xcorr_release(&x);     // synchronises before freeing the template spectra
   return rc;
 }
 
-int vsig_correlate_c64(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
-                       int32_t mode, void* cout, vsig_peak_t* peak) {
+int vsig_correlate_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t na, const void* v,
+                       int64_t nv, int32_t mode, int32_t out_dtype, void* cout,
+                       vsig_peak_t* peak_dev) {
+  if ((dtype != VSIG_DTYPE_C64 && dtype != VSIG_DTYPE_C128) ||
+      (out_dtype != VSIG_DTYPE_C64 && out_dtype != VSIG_DTYPE_C128))
+    return fail(c, VSIG_E_INVALID, "dtype must be VSIG_DTYPE_C64 or VSIG_DTYPE_C128");
+  return correlate_impl(c, dtype == VSIG_DTYPE_C128, a, na, v, nv, mode,
+                        out_dtype == VSIG_DTYPE_C128, cout, peak_dev);
+}
+
+int vsig_correlate_c64_dev(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
+                           int32_t mode, void* cout, vsig_peak_t* peak_dev) {
+  return correlate_impl(c, 0, a, na, v, nv, mode, 0, cout, peak_dev);
+}
+
+int vsig_correlate(vsig_ctx* c, int32_t dtype, const void* a, int64_t na, const void* v,
+                   int64_t nv, int32_t mode, int32_t out_dtype, void* cout, vsig_peak_t* peak) {
   if (!c || !a || !v) return fail(c, VSIG_E_INVALID, "null pointer");
   if (na < 1 || nv < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  if ((dtype != VSIG_DTYPE_C64 && dtype != VSIG_DTYPE_C128) ||
+      (out_dtype != VSIG_DTYPE_C64 && out_dtype != VSIG_DTYPE_C128))
+    return fail(c, VSIG_E_INVALID, "dtype must be VSIG_DTYPE_C64 or VSIG_DTYPE_C128");
+  const size_t es = dtype == VSIG_DTYPE_C128 ? 16 : 8, eo = out_dtype == VSIG_DTYPE_C128 ? 16 : 8;
   const long long nmin = na < nv ? na : nv, nmax = na < nv ? nv : na;
   const long long nout = mode == VSIG_MODE_FULL ? na + nv - 1
                        : mode == VSIG_MODE_VALID ? nmax - nmin + 1 : nmax;
   int rc;
-  if ((rc = ensure_stage(c, 0, (size_t)na * 8)) || (rc = ensure_stage(c, 1, (size_t)nv * 8)) ||
-      (cout && (rc = ensure_stage(c, 2, (size_t)nout * 8))))
+  if ((rc = ensure_stage(c, 0, (size_t)na * es)) || (rc = ensure_stage(c, 1, (size_t)nv * es)) ||
+      (cout && (rc = ensure_stage(c, 2, (size_t)nout * eo))))
     return rc;
-  HIPCHK(c, hipMemcpyAsync(c->stage[0], a, (size_t)na * 8, hipMemcpyHostToDevice, c->stream));
-  HIPCHK(c, hipMemcpyAsync(c->stage[1], v, (size_t)nv * 8, hipMemcpyHostToDevice, c->stream));
-  rc = vsig_correlate_c64_dev(c, c->stage[0], na, c->stage[1], nv, mode, cout ? c->stage[2] : nullptr,
-                              nullptr);
+  HIPCHK(c, hipMemcpyAsync(c->stage[0], a, (size_t)na * es, hipMemcpyHostToDevice, c->stream));
+  HIPCHK(c, hipMemcpyAsync(c->stage[1], v, (size_t)nv * es, hipMemcpyHostToDevice, c->stream));
+  rc = vsig_correlate_dev(c, dtype, c->stage[0], na, c->stage[1], nv, mode, out_dtype,
+                          cout ? c->stage[2] : nullptr, nullptr);
   if (rc) return rc;
-  if (cout) HIPCHK(c, hipMemcpyAsync(cout, c->stage[2], (size_t)nout * 8, hipMemcpyDeviceToHost, c->stream));
+  if (cout) HIPCHK(c, hipMemcpyAsync(cout, c->stage[2], (size_t)nout * eo, hipMemcpyDeviceToHost, c->stream));
   if (peak) HIPCHK(c, hipMemcpyAsync(peak, c->result, sizeof(vsig_peak_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return VSIG_OK;
+}
+
+int vsig_correlate_c64(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
+                       int32_t mode, void* cout, vsig_peak_t* peak) {
+  return vsig_correlate(c, VSIG_DTYPE_C64, a, na, v, nv, mode, VSIG_DTYPE_C64, cout, peak);
 }
 
 // ---------------------------------------------------------------- peak
@@ -861,8 +914,7 @@ int vsig_pfb_c64_dev(vsig_ctx* c, const void* x, int64_t n, const float* h, int3
   int rc = get_twiddles(c, nchan, &tw);
   if (rc) return rc;
   Timed t(c, "pfb");
-  HIPCHK(c, vsig::launch_pfb(nchan, pt, (const float2*)x, n, h, nframes, (float2*)y, tw, c->pfb_variant,
-                             c->pfb_fpg, c->stream));
+  HIPCHK(c, vsig::launch_pfb(nchan, pt, (const float2*)x, n, h, nframes, (float2*)y, tw, c->stream));
   return VSIG_OK;
 }
 
@@ -978,6 +1030,13 @@ int vsig_abs_c64_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, void*
   if (!c || !a || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
   HIPCHK(c, vsig::launch_abs_c64(dtype, a, n, (float2*)out, c->stream));
+  return VSIG_OK;
+}
+
+int vsig_abs_c128_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, void* out) {
+  if (!c || !a || !out) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  HIPCHK(c, vsig::launch_abs_c128(dtype, a, n, (double2*)out, c->stream));
   return VSIG_OK;
 }
 

@@ -11,25 +11,9 @@ namespace vsig {
 // (a bijection on [0, nb)), so the overlap of b and its successor (dispatched
 // at about the same time to the same XCD) hits in L2.
 __device__ __forceinline__ long long xcd_remap(long long b, long long nb) {
-#ifdef VSIG_NO_XCD_REMAP
-  (void)nb;
-  return b;
-#else
   const long long q = nb >> 3, r = nb & 7;
   const long long x = b & 7, i = b >> 3;
   return x * q + (x < r ? x : r) + i;
-#endif
-}
-
-// Block dispatch order of the chain's stages (A/B builds: VSIG_REV_MASK bit 0
-// FIR, bit 1 PSD, bit 2 correlator walk the stream back to front), so a stage
-// starts on the part of the stream the previous one wrote last.
-#ifndef VSIG_REV_MASK
-#define VSIG_REV_MASK 0
-#endif
-template <int STAGE>
-__device__ __forceinline__ unsigned stage_bid() {
-  return (VSIG_REV_MASK & STAGE) ? gridDim.x - 1 - blockIdx.x : blockIdx.x;
 }
 
 enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
@@ -98,26 +82,21 @@ struct PeakPartial {
   double sum_abs2;   // sum |c|^2
 };
 
-// Radices of the plan for N points (N = -16384: the E = 32 plan of 16384).
+// Radices of the plan for N points (N = -1024: the one-wave FIR plan; -512 /
+// -256: the decimating FIR's inverse plans).
 hipError_t plan_info(int N, int* radices, int* npasses);
 // Two-level twiddle table geometry: W_N^m = A[m >> shift] * B[m & (2^shift - 1)],
 // A has `hi` entries, B has 2^shift.
 hipError_t tw2_info(int N, int* shift, int* hi);
 
-// Kernel variants (tuning): bit 0 persistent + register twiddle anchors;
-// bit 1 (M = 16384) E = 32 plan; bit 2 persistent + late prefetch; bit 3
-// two-level LDS twiddle table (one unit per block); bit 4 split re/im LDS
-// exchange; bit 5 (xcorr) partitioned correlation with M = L-point FFTs;
-// bit 6 (xcorr, M = 16384) half-frame kernel: two 8192-point halves through
-// LDS, two blocks per CU (wt = W_M^t table, t < 256).
-struct Variants { int psd, fir, xcorr; };
-
+// Spectrum: nfft >= 4096 two frames per block (anchors, fft_pair), smaller
+// plans several frames per block (LDS twiddles, split exchange; tw = the
+// two-level table, see psd_plan_threads).
 hipError_t launch_psd(int N, const float2* x, long long stride, const float* win, int nperseg,
                       long long hop, float scale, float* out, long long nframes, int shift,
-                      const float2* tw, int variant, hipStream_t st);
-void set_psd_grid_cap(int cap);   // persistent PSD variants: max blocks (0 = all slots)
-// Threads per frame of the spectrum plan for N points (0: no plan); the
-// anchor / pair PSD variants need >= 256 (one frame per block).
+                      const float2* tw, hipStream_t st);
+// Threads per frame of the spectrum plan for N points (0: no plan): >= 256
+// reads the per-pass twiddle table, below the two-level one.
 int psd_plan_threads(int N);
 hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, float2* S,
                                 const float2* tw, hipStream_t st);
@@ -126,37 +105,55 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
                           int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
                           hipStream_t st, const MixArgs* mix = nullptr);
-// Fused FIR (M = 1024, decim 1) -> PSD (nfft = nperseg = hop = 8192), firpsd.hip.
-int fir_psd_seg_hop(int nfft);
-hipError_t launch_fir_psd(int nfft, const float2* x, long long n, long long g0, const float2* Hs,
-                          int ntaps, float2* y, const float* win, float scale, int shift,
-                          float* sxx, long long nframes, const float2* twf, const float2* tws,
-                          int variant, hipStream_t st);
+// Overlap-save FIR, M in {1024, 4096, 8192, 16384} (mix: M = 1024 only).
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
-                         int variant, hipStream_t st, const MixArgs* mix = nullptr);
+                         hipStream_t st, const MixArgs* mix = nullptr);
+// Correlator, M in {4096, 8192, 16384} (16384: half-frame kernel, tw = the
+// 8192-point table, wt = W_M^t for t < 256).
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, const float2* wt,
-                           int variant, hipStream_t st);
-// Partitioned correlation (template halves P0 / P1 of Lp = M / 2 samples).
-hipError_t launch_xcorr_part(int M, const float2* s, long long n, const float2* P0,
-                             const float2* P1, long long off, long long nout, float2* c,
-                             int store_mode, PeakPartial* partials, const float2* tw, int twl,
-                             hipStream_t st);
-// Tuning micro-benchmark: iters FFTs per frame, frames blocks (key: plan key).
+                           hipStream_t st);
+hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan);
+#ifdef VSIG_TUNING
+// Tuning micro-benchmarks: iters FFTs per frame, frames blocks (key: plan key).
 hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const float2* tw, int twl,
                             hipStream_t st);
+hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
+                             hipStream_t st);
+#endif
 hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
                               int nparts, hipStream_t st);
 constexpr int kFinalizeTmp = 1024;   // first-level partials of a two-level finalize
-int os_waves(int M, int variant);    // waves per overlap-save block (partials per unit)
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
                                    PeakPartial* out, PeakPartial* tmp, hipStream_t st);
 
+// refine.hip: exact re-rank of the |c| peak (see the file's header).
+struct RefineArgs {
+  const void* a; long long na;      // np.correlate(a, v) operands (device),
+  const void* v; long long nv;      //   complex128 if c128 else complex64
+  int c128;
+  long long nout, F;                // final outputs; o <-> full index F + o
+  int rev;                          // kernel raw index -> final nout - 1 - raw
+  int from_array;                   // candidates from a stored c64 array c64[nout]
+  const float2* c64;
+  const PeakPartial* parts;         // or from the fused correlator's wave partials
+  long long nparts, hop;
+  int waves, Q, stride;             // wave w of block b: ob + 64 w + l + stride q
+  double eps, eps2;                 // fp32 band, stage-2 band (relative)
+  long long cap_items;
+  void* scratch;                    // refine_scratch_bytes(cap_items, Q)
+  PeakPartial* rec;                 // finalized record (max |c|), updated in place
+  void* out128;                     // optional complex128 c to patch (final space)
+};
+size_t refine_scratch_bytes(long long cap_items, int Q);
+hipError_t launch_refine(const RefineArgs& r, hipStream_t st);
+hipError_t launch_convert_c(int to128, const void* x, long long n, void* y, hipStream_t st);
+
 // pfb.hip: C in {64, 128, 256}, PT in {4, 8, 16}; y frame-major (M x C)
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
-                      float2* y, const float2* tw, int variant, int fpg, hipStream_t st);
+                      float2* y, const float2* tw, hipStream_t st);
 
 // stream_ops.hip
 hipError_t launch_mix_c64(const float2* x, long long n, double w, double sr, long long i0, float2* y,
@@ -166,8 +163,6 @@ hipError_t launch_wv_quantize(const float2* x, long long n, float norm, short* o
 hipError_t launch_planar_to_c64(int mi_type, const void* re, const void* im, long long n, float2* y,
                                 hipStream_t st);
 hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* im, hipStream_t st);
-hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
-                             hipStream_t st);
 
 // analysis.hip
 hipError_t launch_radix_hist(int dtype, const void* a, long long n, const unsigned long long* prefix,
@@ -183,5 +178,6 @@ hipError_t launch_boxcar_same(const double* P, long long n, long long w, double*
 hipError_t launch_db_transform(int dtype, const void* a, long long n, double floor_, void* out,
                                hipStream_t st);
 hipError_t launch_abs_c64(int dtype, const void* a, long long n, float2* out, hipStream_t st);
+hipError_t launch_abs_c128(int dtype, const void* a, long long n, double2* out, hipStream_t st);
 
 }  // namespace vsig

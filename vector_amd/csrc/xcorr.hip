@@ -1,36 +1,40 @@
 // Cross-correlation kernels (gfx950): overlap-save correlation with the fused
-// |c|^2 argmax / sums epilogue (correlate, find_correlation_peak), its
-// half-frame (two blocks per CU) and partitioned-template forms.
+// |c|^2 argmax / sums epilogue (correlate, find_correlation_peak).
+//   M = 16384 (templates of 2049 .. 8192 samples): xcorr_half_kernel, two
+//     8192-point halves through LDS, two blocks per CU;
+//   M = 4096 / 8192 (templates up to 1024 / 2048): xcorr_os_kernel, one frame
+//     per block, persistent with the next segment prefetched.
+// Both use register twiddle anchors (no global loads inside a transform).
 #include "os_common.hpp"
 
 namespace vsig {
 
 // ---------------------------------------------------------------------------
-// Cross-correlation, overlap-save:  c[o] = sum_{k<L} s[o - off + k] * conj(p[k]),
-// o in [0, nout).  off = 0 -> np.correlate 'valid'; off = L-1 -> 'full'.
-// Block b: outputs [b*hop, b*hop + hop), hop <= M - L + 1.
-// Epilogue: optional store of c (store_mode 1) or of conj(c) at nout-1-o
-// (store_mode 2, the swapped argument order of np.correlate), and the block's
-// |c| partial; store_mode bit 4 reports the argmax in the reversed index
-// space (first maximum of the reversed output); bit 8 adds to c instead of
-// storing (templates longer than 8192 run as a sum of template chunks).
+// c[o] = sum_{k<L} s[o - off + k] * conj(p[k]), o in [0, nout).  off = 0 ->
+// np.correlate 'valid'; off = L-1 -> 'full'.  Block b: outputs
+// [b*hop, b*hop + hop), hop <= M - L + 1.
+// store_mode: bits 0-1: 1 store c, 2 store conj(c) at nout-1-o (np.correlate's
+// swapped argument order); bit 2 (4): argmax in the reversed index space;
+// bit 3 (8): add to c instead of storing (templates longer than 8192 run as a
+// sum of template chunks).
+// Partials: one per wave.  Wave w of block b covers the outputs
+//   b*hop + 64 w + l + TF q,   l < 64, q < Q   (Q = E, or 2 E for the half
+// kernel), which refine.hip uses to revisit a wave's outputs.
+// ---------------------------------------------------------------------------
 __device__ __forceinline__ void put_c(float2* p, float2 v, bool accum) {
   *p = accum ? cadd(*p, v) : v;
 }
-// ---------------------------------------------------------------------------
-// Epilogue of one correlation block: |c|^2, block argmax / sums, optional store.
+
 template <class P>
 __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, long long hop,
                                                long long nout, float2* __restrict__ c,
                                                int store_mode, PeakPartial* partials, int t) {
-  constexpr int BT = os_threads<P>();
   const long long ob = b * hop;                         // block's first output
   const long long rem = nout - ob;
   const int lim = rem < hop ? (int)rem : (int)hop;
   const bool rev = store_mode & 4;
   const bool accum = store_mode & 8;
   const int smode = store_mode & 3;
-  // optional store: one uniform branch outside the element loops
   if (smode == 1) {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
@@ -62,91 +66,22 @@ __device__ __forceinline__ void xcorr_epilogue(const float2* v, long long b, lon
     s1 += ok ? __builtin_amdgcn_sqrtf(a2r) : 0.f;   // v_sqrt_f32 (1 ulp), not the IEEE expansion
     s2 += ok ? a2r : 0.f;
   }
-  wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (BT / 64) + (t >> 6));
+  wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
 }
 
-template <class P, int PERSIST>
-__global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void xcorr_os_kernel(
+// Persistent: a block walks blocks b, b + grid, ...; the next segment is
+// loaded behind the (L2-resident) template-spectrum loads, so it lands while
+// the inverse FFT runs (vmcnt retires in issue order).
+template <class P>
+__global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
     const float2* __restrict__ s, long long n, const float2* __restrict__ Ps, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  constexpr int BT = os_threads<P>();
-  static_assert(BT == P::TF, "one frame per block");
-  __shared__ float2 lds[os_lds<P, PERSIST>()];
+  __shared__ float2 lds[P::LDS];
   const int t = threadIdx.x;
-  long long b = PERSIST == 0 || PERSIST >= 3 ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  long long b = blockIdx.x;
   if (b >= nblocks) return;
-
-  if constexpr (PERSIST == 4) {      // one unit per block, LDS twiddles, split exchange
-    float2* t2 = lds + (P::LDS + 1) / 2;
-    float* ldf = reinterpret_cast<float*>(lds);
-    load_tw2<P>(t2, tw, t, BT);
-    float2 v[P::E];
-    load_segment<P>(v, s, b * hop - off, n, t);
-    fft_frame_split<P>(v, ldf, t2, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
-    fft_frame_split<P>(v, ldf, t2, t);
-    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
-    return;
-  }
-  if constexpr (PERSIST == 3) {      // one unit per block, two-level LDS twiddles
-    float2* t2 = lds + P::LDS;
-    load_tw2<P>(t2, tw, t, BT);
-    float2 v[P::E];
-#ifdef VSIG_EXP_NO_LOAD      // timing experiments only (results are wrong)
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = make_float2((float)(t + e), (float)(b & 7));
-#else
-    load_segment<P>(v, s, b * hop - off, n, t);
-#endif
-    fft_frame_t2<P>(v, lds, t2, t);
-#ifdef VSIG_EXP_NO_PS
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), make_float2(0.5f, 0.25f));
-#else
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
-#endif
-    fft_frame_t2<P>(v, lds, t2, t);
-#ifdef VSIG_EXP_NO_EPI
-    float acc = 0.f;
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) acc += v[e].x + v[e].y;
-    if (acc == 12345.f) partials[b].sum_abs = acc;
-#else
-    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
-#endif
-    return;
-  }
-  if constexpr (!PERSIST) {          // one unit per block, table twiddles
-    float2 v[P::E];
-    load_segment<P>(v, s, b * hop - off, n, t);
-    fft_frame<P>(v, lds, tw, t);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
-    fft_frame<P>(v, lds, tw, t);
-    xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
-    return;
-  } else if constexpr (PERSIST == 2) {   // persistent, table twiddles, late prefetch
-    float2 v[P::E];
-    load_segment<P>(v, s, b * hop - off, n, t);
-    for (; b < nblocks; b += gridDim.x) {
-      fft_frame<P>(v, lds, tw, t);
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
-      float2 nv[P::E];
-      const long long nb = b + gridDim.x;
-      fft_frame_hook<P>(v, lds, tw, t, [&] {
-        if (nb < nblocks) load_segment<P>(nv, s, nb * hop - off, n, t);
-      });
-      xcorr_epilogue<P>(v, b, hop, nout, c, store_mode, partials, t);
-#pragma unroll
-      for (int e = 0; e < P::E; ++e) v[e] = nv[e];
-    }
-    return;
-  }
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
   float2 v[P::E];
@@ -155,7 +90,7 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void xc
     fft_frame_anch<P>(v, lds, wa, t);
 #pragma unroll
     for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(v[e]), Ps[out_index<P>(t, e)]);
-    float2 nv[P::E];   // prefetch behind the template-spectrum loads (see fir_os_kernel)
+    float2 nv[P::E];
     const long long nb = b + gridDim.x;
     if (nb < nblocks) load_segment<P>(nv, s, nb * hop - off, n, t);
     fft_frame_anch<P>(v, lds, wa, t);
@@ -166,17 +101,18 @@ __global__ __launch_bounds__(os_threads<P>(), (min_waves<P, PERSIST>())) void xc
 }
 
 // ---------------------------------------------------------------------------
-// Half-frame correlator (variant bit 6): the same overlap-save correlation with
-// M = 2 * P::N points, but the M-point transforms are split by one radix-2
-// step held in registers, so LDS only ever holds one P::N-point half:
+// Half-frame correlator: the same overlap-save correlation with M = 2 * P::N
+// points, the M-point transforms split by one radix-2 step held in registers,
+// so LDS only ever holds one P::N-point half:
 //   forward (DIF):  a[j] = x[j] + x[j+H],  d[j] = (x[j] - x[j+H]) W_M^j,
 //                   X[2k] = FFT_H(a)[k],   X[2k+1] = FFT_H(d)[k]       (H = M/2)
 //   inverse (DIT):  r[n] = E[n] + W_M^n O[n],  r[n+H] = E[n] - W_M^n O[n],
 //                   E / O = FFT_H of the even / odd bins of conj(X) Ps.
-// Every thread keeps the whole frame in VGPRs (2 * P::E values), the LDS
+// Every thread keeps the whole frame in VGPRs (2 * P::E values); the LDS
 // exchange buffer is 69 KB at M = 16384, so two blocks share a CU and one
-// block's loads / barriers / LDS exchanges overlap the other's butterflies
-// (the one-block-per-CU M = 16384 kernel exposes all of them).
+// block's loads / barriers / LDS exchanges overlap the other's butterflies.
+// The two halves go through fft_pair (LDS stores of one half overlap the
+// other's butterflies), twiddles from register anchors.
 // With P palindromic, in_index == out_index = t + (e / R0) TF + (e % R0) N / R0,
 // so W_M^j = W_M^t * W_64^K(e): one per-thread twiddle (table wt) and a
 // compile-time 64th root per element.
@@ -272,12 +208,7 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
   wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
 }
 
-// TW: twiddle source of the passes: 0 the global per-pass table, 1 the
-// two-level LDS table, 2 per-thread register anchors (no loads inside the
-// transforms; see TwAnchors in fft_engine.hpp).  PAIR: the two halves go
-// through fft_pair (LDS stores of one half overlap the other's butterflies)
-// instead of two back-to-back fft_frame calls.
-template <class P, int TW, int PAIR>
+template <class P>
 __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
@@ -287,36 +218,18 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
   constexpr int M = 2 * P::N;
   static_assert(P::TF % (M / 64) == 0 && (P::N / P::R[0]) % (M / 64) == 0,
                 "per-element split twiddles must be 64th roots of unity");
-  __shared__ float2 lds[P::LDS + (TW == 1 ? tw2_size<P>() : 0)];
+  __shared__ float2 lds[P::LDS];
   const int t = threadIdx.x;
-  const long long b = xcd_remap(stage_bid<4>(), gridDim.x);
+  const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (b >= nblocks) return;
-  float2* t2 = lds + P::LDS;
-  if constexpr (TW == 1) load_tw2<P>(t2, tw, t, P::TF);
-  float2 wa[TW == 2 ? nanch_total<P>() : 1];
-  if constexpr (TW == 2) load_anchors<P>(wa, tw, t);
-  auto fft = [&](float2* v) {
-    if constexpr (TW == 1) fft_frame_t2<P>(v, lds, t2 + opaque_zero(), t);
-    else if constexpr (TW == 2) fft_frame_anch<P>(v, lds, wa, t);
-    else fft_frame<P>(v, lds, tw, t);
-  };
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
   auto fft2 = [&](float2* x, float2* y) {
-    if constexpr (PAIR) {
-      if constexpr (TW == 1) fft_pair<P>(x, y, lds, TwLds{t2 + opaque_zero()}, t);
-      else if constexpr (TW == 2) { launder_anchors<P>(wa); fft_pair<P>(x, y, lds, TwAnchors{wa}, t); }
-      else fft_pair<P>(x, y, lds, TwTable{tw + opaque_zero()}, t);
-    } else {
-      fft(x);
-      fft(y);
-    }
+    launder_anchors<P>(wa);
+    fft_pair<P>(x, y, lds, TwAnchors{wa}, t);
   };
   float2 a[P::E], d[P::E];
-#ifdef VSIG_EXP_NO_LOAD      // timing experiments only (results are wrong)
-#pragma unroll
-  for (int e = 0; e < P::E; ++e) { a[e] = make_float2((float)(t + e), (float)(b & 7)); d[e] = make_float2((float)e, 1.f); }
-#else
   load_halves<P>(a, d, s, b * hop - off, n, t);
-#endif
   const float2 w = wt[t];
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
@@ -327,11 +240,7 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
   fft2(a, d);
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
-#ifdef VSIG_EXP_NO_PS
-    const float4 p = make_float4(0.5f, 0.25f, 0.125f, 0.5f);
-#else
     const float4 p = Ps2[out_index<P>(t, e)];
-#endif
     a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
     d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
   }
@@ -343,137 +252,42 @@ __global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
   });
-#ifdef VSIG_EXP_NO_EPI
-  float acc = 0.f;
-#pragma unroll
-  for (int e = 0; e < P::E; ++e) acc += a[e].x + a[e].y + d[e].x + d[e].y;
-  if (acc == 12345.f) partials[b].sum_abs = acc;
-#else
   xcorr_half_epilogue<P>(a, d, b, hop, nout, c, store_mode, partials, t);
-#endif
-}
-
-// ---------------------------------------------------------------------------
-// Partitioned cross-correlation (uniformly partitioned overlap-save): the
-// template is cut into two halves of Lp = M/2 samples; hop j's outputs are
-//   c[j*Lp + i] = IFFT( X_j conj(P0) + X_{j+1} conj(P1) )[i],   i < Lp,
-// X_j = FFT_M(s[j*Lp - off ...]).  A block walks a contiguous run of hops,
-// carrying X_{j+1} in registers into hop j+1, so each hop costs one forward and
-// one inverse M-point FFT: M = L-point FFTs (4 blocks / CU at L = 4096) instead
-// of the 4L-point FFTs plain overlap-save needs for the same efficiency.
-// ---------------------------------------------------------------------------
-template <class P, int TWL>
-__global__ __launch_bounds__(os_threads<P>(), 2) void xcorr_part_kernel(
-    const float2* __restrict__ s, long long n, const float2* __restrict__ P0,
-    const float2* __restrict__ P1, long long off, long long nout, int Lp, long long nhops,
-    long long hpb, float2* __restrict__ c, int store_mode, PeakPartial* __restrict__ partials,
-    const float2* __restrict__ tw) {
-  static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  constexpr int BT = os_threads<P>();
-  __shared__ float2 lds[P::LDS + (TWL ? tw2_size<P>() : 0)];
-  const int t = threadIdx.x;
-  const long long j0 = (long long)blockIdx.x * hpb;
-  const long long j1 = j0 + hpb < nhops ? j0 + hpb : nhops;
-  if (j0 >= j1) return;
-  float2* t2 = lds + P::LDS;
-  if constexpr (TWL) load_tw2<P>(t2, tw, t, BT);
-  auto fft = [&](float2* v, int tt) {
-    if constexpr (TWL) fft_frame_t2<P>(v, lds, t2, tt);
-    else fft_frame<P>(v, lds, tw, tt);
-  };
-  float2 xn[P::E];                      // X_{j+1} of the previous hop
-  load_segment<P>(xn, s, j0 * Lp - off, n, t);
-  fft(xn, t);
-  for (long long j = j0; j < j1; ++j) {
-    // An opaque copy of the thread index: keeps the (loop-invariant) LDS and
-    // twiddle address arithmetic of the three FFTs inside the loop instead of
-    // hoisted into hundreds of live VGPRs.
-    const int tt = t + opaque_zero();
-    float2 v[P::E];
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = cmul(cconj(xn[e]), P0[out_index<P>(tt, e)]);
-    load_segment<P>(xn, s, (j + 1) * Lp - off, n, tt);
-    fft(xn, tt);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const float2 a = cmul(cconj(xn[e]), P1[out_index<P>(tt, e)]);
-      v[e] = cadd(v[e], a);
-    }
-    fft(v, tt);
-    xcorr_epilogue<P>(v, j, Lp, nout, c, store_mode, partials, tt);
-  }
-}
-
-template <class PL, int PERSIST>
-void launch_xcorr_t(const float2* s, long long n, const float2* Ps, long long off, long long nout,
-                    long long hop, float2* c, int store_mode, PeakPartial* partials,
-                    long long nblocks, const float2* tw, hipStream_t st) {
-  const long long grid =
-      (PERSIST == 1 || PERSIST == 2)
-          ? persistent_grid(xcorr_os_kernel<PL, PERSIST>, os_threads<PL>(), nblocks) : nblocks;
-  hipLaunchKernelGGL((xcorr_os_kernel<PL, PERSIST>), dim3((unsigned)grid),
-                     dim3(os_threads<PL>()), 0, st, s, n, Ps, off, nout, hop, c, store_mode,
-                     partials, nblocks, tw);
 }
 
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
-                           PeakPartial* partials, const float2* tw, const float2* wt, int variant,
+                           PeakPartial* partials, const float2* tw, const float2* wt,
                            hipStream_t st) {
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
-  if ((variant & 64) && M == 16384) {   // half-frame kernel, two blocks per CU
-    auto k = (variant & 128)
-                 ? ((variant & 8)   ? xcorr_half_kernel<Plan8192, 1, 1>
-                    : (variant & 1) ? xcorr_half_kernel<Plan8192, 2, 1>
-                                    : xcorr_half_kernel<Plan8192, 0, 1>)
-                 : ((variant & 8)   ? xcorr_half_kernel<Plan8192, 1, 0>
-                    : (variant & 1) ? xcorr_half_kernel<Plan8192, 2, 0>
-                                    : xcorr_half_kernel<Plan8192, 0, 0>);
-    hipLaunchKernelGGL(k, dim3((unsigned)nblocks), dim3(Plan8192::TF), 0, st, s, n,
-                       reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
+  if (M == 16384) {
+    hipLaunchKernelGGL(xcorr_half_kernel<Plan8192>, dim3((unsigned)nblocks), dim3(Plan8192::TF), 0,
+                       st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
                        partials, nblocks, tw, wt);
     return hipGetLastError();
   }
-  VSIG_OS_SWITCH(M, variant, {
-    if (variant & 16) launch_xcorr_t<PL, 4>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
-    else if (variant & 8) launch_xcorr_t<PL, 3>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
-    else if (variant & 4) launch_xcorr_t<PL, 2>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
-    else if (variant & 1) launch_xcorr_t<PL, 1>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
-    else launch_xcorr_t<PL, 0>(s, n, Ps, off, nout, hop, c, store_mode, partials, nblocks, tw, st);
-  });
+  auto run = [&](auto plan) {
+    using PL = decltype(plan);
+    auto k = xcorr_os_kernel<PL>;
+    const long long grid = persistent_grid(k, PL::TF, nblocks);
+    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(PL::TF), 0, st, s, n, Ps, off, nout, hop, c,
+                       store_mode, partials, nblocks, tw);
+  };
+  if (M == 4096) run(Plan4096{});
+  else if (M == 8192) run(Plan8192{});
+  else return hipErrorInvalidValue;
   return hipGetLastError();
 }
 
-hipError_t launch_xcorr_part(int M, const float2* s, long long n, const float2* P0,
-                             const float2* P1, long long off, long long nout, float2* c,
-                             int store_mode, PeakPartial* partials, const float2* tw, int twl,
-                             hipStream_t st) {
-  if (nout <= 0) return hipSuccess;
-  const int Lp = M / 2;
-  const long long nhops = (nout + Lp - 1) / Lp;
-  VSIG_OS_SWITCH(M, 0, {
-    auto k = twl ? xcorr_part_kernel<PL, 1> : xcorr_part_kernel<PL, 0>;
-    const long long g = persistent_grid(k, os_threads<PL>(), nhops);
-    const long long hpb = (nhops + g - 1) / g;
-    const long long grid = (nhops + hpb - 1) / hpb;
-    hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(os_threads<PL>()), 0, st, s, n, P0, P1,
-                       off, nout, Lp, nhops, hpb, c, store_mode, partials, tw);
-  });
-  return hipGetLastError();
-}
-
-int os_waves(int M, int variant) {
-  switch (M) {
-    case 1024: return os_threads<Plan1024s>() / 64;
-    case 2048: return os_threads<Plan2048s>() / 64;
-    case 4096: return os_threads<Plan4096>() / 64;
-    case 8192: return os_threads<Plan8192>() / 64;
-    case 16384:
-      if (variant & 64) return Plan8192::TF / 64;
-      return (variant & 2) ? os_threads<Plan16384w>() / 64 : os_threads<Plan16384>() / 64;
-    default: return 0;
-  }
+// Wave geometry of the correlator's partials (see the header comment):
+// waves per block, rows Q and their stride; twiddle plan size.
+hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan) {
+  if (M == 16384) { *waves = Plan8192::TF / 64; *Q = 2 * Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
+  else if (M == 8192) { *waves = Plan8192::TF / 64; *Q = Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
+  else if (M == 4096) { *waves = Plan4096::TF / 64; *Q = Plan4096::E; *stride = Plan4096::TF; *plan = 4096; }
+  else return hipErrorInvalidValue;
+  return hipSuccess;
 }
 
 }  // namespace vsig

@@ -31,7 +31,8 @@ from .windows import get_window
 
 __all__ = ["spectrum", "filter", "fir_filter", "correlate", "correlate_peak",
            "cross_correlate_signals", "find_correlation_peak",
-           "find_packet_location_in_vector", "FirFilter", "Correlator", "peak_stats"]
+           "find_packet_location_in_vector", "FirFilter", "Correlator", "peak_stats",
+           "refine_status"]
 
 PEAK_BYTES = 32  # sizeof(vsig_peak_t)
 
@@ -258,24 +259,6 @@ class FirFilter:
         """Overlap-save block size the library chose for these taps."""
         return int(self.ctx.lib.vsig_fir_block(self.h))
 
-    def fir_psd(self, x: torch.Tensor, nhist: int, out: torch.Tensor, win: torch.Tensor,
-                nfft: int, scale: float, sxx: torch.Tensor, shift: int = 0) -> None:
-        """Fused filter + spectrum (decim 1, nfft 8192): out as __call__,
-        sxx (frame-major float32, len(out) // nfft frames) as vsig_psd_c64_dev
-        of out with nperseg = hop = nfft."""
-        self.ctx.bind_stream()
-        _check_dev(x, 1, torch.complex64, "filter input", self.ctx.device)
-        n = int(x.shape[0]) - int(nhist)
-        if n < 1 or nhist < 0:
-            raise ValueError("filter: need len(x) > nhist >= 0")
-        nframes = n // int(nfft)
-        _check_dev(out, n, torch.complex64, "filter output", self.ctx.device)
-        _check_dev(win, int(nfft), torch.float32, "window", self.ctx.device)
-        _check_dev(sxx, nframes * int(nfft), torch.float32, "spectrum output", self.ctx.device)
-        self.ctx.check(self.ctx.lib.vsig_fir_psd_exec_dev(
-            self.h, _ptr(x), int(nhist), n, _ptr(out), n, _ptr(win), int(nfft), float(scale),
-            int(shift), _ptr(sxx), nframes), "filter+spectrum")
-
     def __del__(self):
         try:
             if self.h:
@@ -356,35 +339,89 @@ def _check_mode(mode):
         raise ValueError(f"mode must be one of 'full', 'valid', 'same' (got {mode!r})")
 
 
-def _correlate_dev(a, v, mode, want_array, ctx):
-    """np.correlate(a, v, mode) on the GPU; returns (c tensor or None, peak buffer, nout)."""
-    ad, vd = _device_c64(a, ctx), _device_c64(v, ctx)
+def _is_c128(x) -> bool:
+    """Does the reference's complex128 upcast (utils.py:1279-1282) change x's
+    values?  complex64 / float32 data upcast exactly (the complex64 path is
+    then numpy's arithmetic on the same values); wider dtypes keep 128 bits."""
+    if _is_dev(x):
+        return x.dtype in (torch.complex128, torch.float64, torch.int64, torch.int32)
+    dt = np.asarray(x).dtype
+    return not (dt == np.complex64 or dt == np.float32 or dt == np.float16
+                or dt == np.int8 or dt == np.uint8 or dt == np.int16 or dt == np.uint16)
+
+
+def _device_c128(x, ctx):
+    if _is_dev(x):
+        t = x if x.is_cuda else x.to(f"cuda:{ctx.device}")
+        return t.to(torch.complex128).contiguous()
+    a = np.ascontiguousarray(np.asarray(x), dtype=np.complex128)
+    if a.ndim != 1:
+        raise ValueError("vector_amd works on 1-D signals")
+    return torch.from_numpy(a).to(f"cuda:{ctx.device}")
+
+
+def _correlate_dev(a, v, mode, want_array, ctx, out128=False):
+    """np.correlate(a, v, mode) on the GPU; returns (c tensor or None, peak
+    buffer, nout).  complex128 operands (or any input whose complex128 upcast
+    is not exact) go to the library as complex128: the FFT pass runs in
+    complex64, the argmax refine (refine.hip) in the operands' precision.
+    out128: c is returned as complex128 with the refined outputs patched in."""
+    in128 = _is_c128(a) or _is_c128(v)
+    conv = _device_c128 if in128 else _device_c64
+    ad, vd = conv(a, ctx), conv(v, ctx)
     na, nv = int(ad.shape[0]), int(vd.shape[0])
     if na == 0:
         raise ValueError("a cannot be empty")
     if nv == 0:
         raise ValueError("v cannot be empty")
     nout = _corr_len(mode, na, nv)
-    c = torch.empty(nout, dtype=torch.complex64, device=ad.device) if want_array else None
+    odt = torch.complex128 if out128 else torch.complex64
+    c = torch.empty(nout, dtype=odt, device=ad.device) if want_array else None
     pk = _peak_buffer(ctx)
-    ctx.check(ctx.lib.vsig_correlate_c64_dev(ctx.h, _ptr(ad), na, _ptr(vd), nv,
-                                             _lib.MODES[mode], _ptr(c) if c is not None else None,
-                                             _ptr(pk)), "correlate")
+    ctx.check(ctx.lib.vsig_correlate_dev(ctx.h, _lib.DTYPES["c128" if in128 else "c64"], _ptr(ad),
+                                         na, _ptr(vd), nv, _lib.MODES[mode],
+                                         _lib.DTYPES["c128" if out128 else "c64"],
+                                         _ptr(c) if c is not None else None, _ptr(pk)),
+              "correlate")
     return c, pk, nout
+
+
+def refine_status(ctx=None):
+    """(status, candidates) of the last correlation's argmax refine:
+    0 refined, 1 skipped (more candidates than the 'refine_cap' option),
+    2 no refine pass ran."""
+    ctx = ctx or _lib.get_context()
+    st, nc = C.c_int32(), C.c_int64()
+    ctx.check(ctx.lib.vsig_refine_status(ctx.h, C.byref(st), C.byref(nc)), "refine_status")
+    return int(st.value), int(nc.value)
+
+
+def _warn_unrefined(ctx):
+    st, nc = refine_status(ctx)
+    if st == 1:
+        warnings.warn(f"correlation argmax left at fp32 accuracy: {nc} candidate waves within the "
+                      f"refine band exceed the 'refine_cap' option", RuntimeWarning, stacklevel=3)
 
 
 def cross_correlate_signals(signal1, signal2, mode="full"):
     """utils.py:1258-1295: ``np.correlate(signal2, signal1, mode)`` and the lag
-    axis.  numpy inputs -> complex128 numpy (GPU computes complex64)."""
+    axis.  numpy inputs -> complex128 numpy: the FFT pass runs in complex64, the
+    outputs within the refine band of the peak are recomputed by direct sums
+    in double precision (find_correlation_peak over the result then agrees
+    with numpy's argmax); elsewhere complex64 accuracy."""
     _check_mode(mode)
     ctx = _lib.get_context()
-    c, _, _ = _correlate_dev(signal2, signal1, mode, True, ctx)
+    dev = _is_dev(signal1) or _is_dev(signal2)
+    out128 = (not dev) or _is_c128(signal1) or _is_c128(signal2)
+    c, _, _ = _correlate_dev(signal2, signal1, mode, True, ctx, out128=out128)
     l1 = int(signal1.shape[0]) if _is_dev(signal1) else len(signal1)
     l2 = int(signal2.shape[0]) if _is_dev(signal2) else len(signal2)
     lags = _lags(mode, l1, l2)
-    if _is_dev(signal1) or _is_dev(signal2):
+    if dev:
         return c, lags
-    return c.cpu().numpy().astype(np.complex128), lags
+    out = c.cpu().numpy()
+    _warn_unrefined(ctx)
+    return out, lags
 
 
 correlate = cross_correlate_signals
@@ -436,6 +473,7 @@ def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
     ctx = _lib.get_context()
     _, pk, nout = _correlate_dev(signal2, signal1, mode, False, ctx)
     peak, idx, s1, s2 = _read_peak(pk)
+    _warn_unrefined(ctx)
     l1 = int(signal1.shape[0]) if _is_dev(signal1) else len(signal1)
     l2 = int(signal2.shape[0]) if _is_dev(signal2) else len(signal2)
     if mode == "full":
@@ -451,8 +489,10 @@ def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
 
 
 class Correlator:
-    """Streaming sync detector: a fixed template, correlated against long
-    device-resident streams with the |c| argmax fused in the kernel."""
+    """Streaming sync detector: a fixed template (any length; > 8192 samples
+    runs as one pass per 8192-sample chunk), correlated against long
+    device-resident streams with the |c| argmax fused in the kernel and
+    refined (refine.hip) -- all asynchronous on the current stream."""
 
     def __init__(self, template, device: int | None = None):
         t = np.ascontiguousarray(np.asarray(template).ravel(), dtype=np.complex64)
@@ -461,12 +501,6 @@ class Correlator:
         self.ctx = _lib.get_context(device)
         self.L = int(t.size)
         self.h = None
-        self.tmpl = None
-        if self.L > 8192:
-            # longer templates: the general correlation's chunked path (one
-            # pass per 8192-sample template chunk, accumulated; host-synchronous)
-            self.tmpl = torch.from_numpy(t).to(f"cuda:{self.ctx.device}")
-            return
         h = C.c_void_p()
         self.ctx.check(self.ctx.lib.vsig_xcorr_create(self.ctx.h, t.ctypes.data_as(C.c_void_p),
                                                       self.L, C.byref(h)), "vsig_xcorr_create")
@@ -488,13 +522,8 @@ class Correlator:
         if peak is None:
             peak = _peak_buffer(self.ctx)
         _check_dev(peak, 4, torch.float64, "peak record", self.ctx.device)
-        if self.tmpl is not None:
-            self.ctx.check(self.ctx.lib.vsig_correlate_c64_dev(
-                self.ctx.h, _ptr(s), ns, _ptr(self.tmpl), self.L, _lib.MODES[mode],
-                _ptr(out) if out is not None else None, _ptr(peak)), "xcorr (long template)")
-            return out, peak
         self.ctx.check(self.ctx.lib.vsig_xcorr_exec_dev(
-            self.h, _ptr(s), int(s.shape[0]), _lib.MODES[mode],
+            self.h, _ptr(s), ns, _lib.MODES[mode],
             _ptr(out) if out is not None else None, _ptr(peak)), "xcorr")
         return out, peak
 

@@ -51,9 +51,6 @@ class ChainConfig:
     sample_rate: float = 1.0     # phase from the global sample index (utils.py:120-127)
     one_stream: bool = True      # pipeline == 1: all stages on the caller's stream (the PSD and
                                  # correlator do not overlap anyway; saves the cross-stream waits)
-    fuse: bool = False           # FIR + PSD in one launch where the backend has it (decim 1,
-                                 # one sub-chunk): the PSD re-reads the filtered stream from cache
-                                 # (measured slower than two launches on MI355X: DESIGN.md §4)
 
     def validate(self, world: int):
         ny = self.n_local // self.decim
@@ -137,14 +134,6 @@ class HipBackend:
         self.fir(x_ext, out=y, nhist=nhist, freq_shift=self.freq_shift,
                  sample_rate=self.sample_rate, i0=i0)
 
-    def can_fuse(self, cfg):
-        return (cfg.decim == 1 and not cfg.freq_shift and self.nfft == 8192 and self.fir.ntaps <= 342
-                and self.fir.block == 1024)
-
-    def fir_psd_into(self, x_ext, nhist, y, sxx):
-        """FIR (decim 1) and the PSD of its output in one launch."""
-        self.fir.fir_psd(x_ext, nhist, y, self.win, self.nfft, self.scale, sxx)
-
     def psd_into(self, y, sxx):
         ctx = self.ctx
         ctx.bind_stream()
@@ -190,8 +179,6 @@ class StreamChain:
         self.sxx = backend.empty((self.ny // cfg.nfft) * cfg.nfft, torch.float32)
         self.recs = backend.empty(4 * cfg.pipeline, torch.float64).view(cfg.pipeline, 4)
         self.peak_rows = None
-        self.fused = (cfg.fuse and cfg.pipeline == 1 and not cfg.serial and cfg.decim == 1
-                      and hasattr(backend, "fir_psd_into") and backend.can_fuse(cfg))
 
     @property
     def x(self):
@@ -230,18 +217,12 @@ class StreamChain:
         """FIR of sub-chunk 0 with the left-halo exchange hidden behind it:
         outputs from a decimation-aligned s >= ntaps-1 on need only the rank's
         own samples and are filtered while the halo is in flight; the first
-        s outputs follow once it has landed.  Fused chains (FIR + PSD in one
-        launch) split at a frame boundary s >= ntaps-1 instead."""
+        s outputs follow once it has landed."""
         r, w, hist, n = self.rank, self.world, self.hist, self.cfg.n_local
         D = self.cfg.decim
-        if self.fused:
-            nfft = self.cfg.nfft
 
-            def run(a, b):                       # outputs [a, b) (frame-aligned)
-                be.fir_psd_into(self.x_ext[a: b + hist], hist, self.y_ext[a: b], self.sxx[a: b])
-        else:
-            def run(a, b):
-                self._fir(be, a, b, self.y_ext[a // D: b // D])
+        def run(a, b):
+            self._fir(be, a, b, self.y_ext[a // D: b // D])
         if not (w > 1 and hist > 0):
             run(0, nk)
             return
@@ -249,7 +230,7 @@ class StreamChain:
                                     r + 1 if r < w - 1 else None,
                                     self.x_ext[: hist] if r > 0 else None,
                                     r - 1 if r > 0 else None)
-        s = -(-hist // nfft) * nfft if self.fused else -(-hist // D) * D
+        s = -(-hist // D) * D
         if s < nk:
             run(s, nk)
         self._exchange_wait(reqs)
@@ -281,10 +262,9 @@ class StreamChain:
                                    r + 1 if r < w - 1 else None)
                     ev_halo = _record(be)
         for k in range(K):
-            if not self.fused:
-                with _lane(be, "psd"):          # 4. PSD of sub-chunk k
-                    _wait(be, ev_fir[k])
-                    be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
+            with _lane(be, "psd"):              # 4. PSD of sub-chunk k
+                _wait(be, ev_fir[k])
+                be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
             if L:                               # 5. sync correlation of sub-chunk k
                 with _lane(be, "xcorr"):
                     last = k == K - 1
@@ -317,8 +297,7 @@ class StreamChain:
                                         r - 1 if r > 0 else None,
                                         self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
                                         r + 1 if r < w - 1 else None)
-        if not self.fused:
-            be.psd_into(self.y_ext[: ny], self.sxx)
+        be.psd_into(self.y_ext[: ny], self.sxx)
         if L:
             self._exchange_wait(reqs)
             halo = (L - 1) if r < w - 1 else 0

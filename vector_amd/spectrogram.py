@@ -97,7 +97,7 @@ def create_spectrogram(sig, sr, center_freq=0, max_samples=2_000_000, time_resol
 
     try:                                                              # utils.py:279-313
         freqs, times, Sxx = stft(p["window"], p["nperseg"], p["noverlap"], p["nfft"])
-    except ValueError:   # what scipy raises for these arguments (e.g. nfft < nperseg)
+    except (ValueError, NotImplementedError):   # the reference catches any Exception
         ws = min(256, p["nsig"])
         freqs, times, Sxx = stft("hann", ws, ws // 2, 512)
     if _all_zero(Sxx):                                                # utils.py:316-347
