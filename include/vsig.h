@@ -78,6 +78,10 @@ const char* vsig_last_error(const vsig_ctx* ctx);
 /* hip_stream: the hipStream_t to enqueue on; NULL is the default (null)
  * stream.  A new context starts on a private non-blocking stream. */
 int vsig_set_stream(vsig_ctx* ctx, void* hip_stream);
+/* The hipStream_t the context enqueues on. */
+void* vsig_get_stream(vsig_ctx* ctx);
+/* Copy bytes between device or host buffers, ordered on the context's stream. */
+int vsig_copy_dev(vsig_ctx* ctx, void* dst, const void* src, int64_t bytes);
 int vsig_synchronize(vsig_ctx* ctx);
 /* Options of the correlators' exact-argmax refine pass (refine.hip):
  *   "refine"          1 (default): after every correlation, the outputs whose
@@ -108,7 +112,8 @@ int vsig_timing_read(vsig_ctx* ctx, const char* kernel, double* total_ms, int64_
 int vsig_timing_reset(vsig_ctx* ctx);
 
 /* ---- spectrum: Sxx[f, k] = |sum_{i<nperseg} w[i] x[f*hop + i] e^{-2 pi j k i / nfft}|^2 * scale
- * nfft: power of two in [64, 16384]; nframes = (n - nperseg) / hop + 1;
+ * nfft: power of two in [64, 2^28] (above 16384: four-step FFT per frame);
+ * nframes = (n - nperseg) / hop + 1;
  * sxx is frame-major float32 [nframes][nfft] (Sxx of scipy is its transpose);
  * shift = 1 stores bin k at (k + nfft/2) % nfft (np.fft.fftshift).
  * _dev only: stride reads sample i at x[i*stride] (n counts strided samples),
@@ -174,6 +179,27 @@ int vsig_correlate_c64_dev(vsig_ctx* ctx, const void* a, int64_t na, const void*
 int vsig_correlate_c64(vsig_ctx* ctx, const void* a, int64_t na, const void* v, int64_t nv,
                        int32_t mode, void* c, vsig_peak_t* peak);
 
+/* ---- transforms of any length (bigfft.hip: four-step FFT on the in-LDS engine
+ * for powers of two above 16384, Bluestein / chirp-z for every other length,
+ * up to 2^27 points; complex64 arithmetic).
+ * vsig_dft_dev: batch frames of n contiguous samples, y[f][k] = sum_j x[f][j]
+ *   e^{-+2 pi i jk/n} (inverse: + and 1/n, numpy.fft's convention).
+ * vsig_resample_dev: scipy.signal.resample(x, num) as resample_signal calls it
+ *   (utils.py:107-118): spectrum of x, its bins copied / the Nyquist bin split
+ *   or folded into num bins, inverse transform, * num / n; y complex64[num]
+ *   (real_input: imaginary part 0, scipy's rfft path).
+ * vsig_filter_channel_dev: split_channels.filter_channel (vector_analyzer/
+ *   split_channels.py:15-44) as written, CENTER_FREQ 5230 MHz: brick-wall mask
+ *   on fftfreq(n, 1/sr) * sr + CENTER_FREQ, the negative half replaced by the
+ *   conjugate mirror of the masked non-negative half, inverse FFT, real part
+ *   (y float64[n]).  Odd n > 1: VSIG_E_INVALID (numpy's shape mismatch). */
+int vsig_dft_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t n, int64_t batch,
+                 int32_t inverse, int32_t out_dtype, void* y);
+int vsig_resample_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t n, int64_t num,
+                      int32_t real_input, void* y);
+int vsig_filter_channel_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t n,
+                            double center_freq, double sample_rate, double bandwidth, double* y);
+
 /* ---- |c| reduction in double precision over an array of dtype VSIG_DTYPE_*:
  * index of the first max of |c|, the max, sum |c|, sum |c|^2. */
 int vsig_peak_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev);
@@ -229,6 +255,75 @@ int vsig_boxcar_energy_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t 
 int vsig_db_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, double floor_, void* out);
 int vsig_abs_c64_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, void* out);
 int vsig_abs_c128_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, void* out);
+
+/* ---- time-chunk shard of the streaming chain (chain.hip; the C form of
+ * vector_amd/shard.py StreamChain; reference precedent: the
+ * overlapped chunking of heavy_packet_optimizer.py:114-152).  Rank r of world
+ * owns input samples [r n, (r+1) n) of one capture; per step: left halo
+ * (ntaps-1 input samples from rank r-1) -> FIR + decimate -> right halo (L-1
+ * filtered samples from rank r+1) -> PSD (nfft, hop nfft) -> valid
+ * correlation with the template + exact peak -> all-gather of the 32-byte
+ * peak records.  Results equal one chain over the whole capture.
+ * n must be a multiple of nfft * decim; taps / tmpl complex64 host arrays;
+ * window float32[nfft] host; psd_scale = 1 / sum(window)^2 for 'spectrum'
+ * scaling; tmpl = NULL: no sync stage. */
+typedef struct vsig_chain_config {
+  int64_t n_local;
+  const void* taps;
+  int32_t ntaps;
+  int32_t decim;
+  int32_t nfft;
+  const float* window;
+  float psd_scale;
+  const void* tmpl;
+  int64_t L;
+} vsig_chain_config;
+
+/* How ranks exchange: sendrecv sends send_bytes of device memory to rank dst
+ * and receives recv_bytes into recv from rank src (dst / src < 0: none),
+ * ordered on hip_stream; allgather gathers `bytes` from every rank into recv
+ * (world * bytes, rank order).  Return 0 on success. */
+typedef struct vsig_transport {
+  void* user;
+  int (*sendrecv)(void* user, const void* send, int64_t send_bytes, int32_t dst, void* recv,
+                  int64_t recv_bytes, int32_t src, void* hip_stream);
+  int (*allgather)(void* user, const void* send, void* recv, int64_t bytes, void* hip_stream);
+} vsig_transport;
+
+typedef struct vsig_chain vsig_chain;
+/* tr may be NULL for world = 1.  The chain enqueues on ctx's stream. */
+int vsig_chain_create(vsig_ctx* ctx, const vsig_chain_config* cfg, int32_t rank, int32_t world,
+                      const vsig_transport* tr, vsig_chain** out);
+void vsig_chain_free(vsig_chain* chain);
+const char* vsig_chain_last_error(const vsig_chain* chain);
+/* Device complex64[n_local]: this rank's input chunk (fill before a step). */
+void* vsig_chain_input(vsig_chain* chain);
+int vsig_chain_step(vsig_chain* chain);
+/* The global peak of the last step (index in the whole filtered, decimated
+ * capture; sums over all nout outputs); synchronises. */
+int vsig_chain_result(vsig_chain* chain, vsig_peak_t* peak, int64_t* nout);
+/* This rank's filtered stream (complex64[n]) and spectra (frame-major float32
+ * [nframes][nfft]) on the device. */
+const void* vsig_chain_filtered(const vsig_chain* chain, int64_t* n);
+const float* vsig_chain_spectra(const vsig_chain* chain, int64_t* nframes);
+
+/* RCCL over xGMI as the transport (librccl resolved at run time: an RCCL
+ * already in the process -- e.g. torch's -- is shared; VSIG_RCCL_LIB names
+ * another).  comm is an ncclComm_t; vsig_rccl_comm_init makes one per rank
+ * from a unique id that rank 0 creates and the launcher distributes. */
+int vsig_rccl_available(void);
+int vsig_rccl_unique_id(char id[128]);
+int vsig_rccl_comm_init(int32_t world, int32_t rank, const char id[128], int32_t device, void** comm);
+int vsig_rccl_comm_destroy(void* comm);
+int vsig_rccl_transport(void* comm, vsig_transport* out);
+
+/* In-process loopback transport: ranks as host threads of one process (one
+ * context each), halos copied device to device -- several ranks on one GPU
+ * for tests, or ranks on the GPUs of one process. */
+typedef struct vsig_loopback vsig_loopback;
+int vsig_loopback_create(int32_t world, vsig_loopback** out);
+void vsig_loopback_free(vsig_loopback* lb);
+int vsig_loopback_transport(vsig_loopback* lb, int32_t rank, vsig_transport* out);
 
 #ifdef __cplusplus
 }

@@ -106,9 +106,10 @@ def test_near_tie_below_fp32_resolution(gpu, ratio):
     100x below the fp32 correlation's resolution): the larger one wins."""
     L, n = 2048, 200_000
     pre = ref.qpsk_preamble(L, seed=9)
-    s = (0.01 * ref.synth_iq(n, seed=10)).astype(np.complex128)
+    s = np.zeros(n, np.complex128)                    # noise-free around the copies
+    s[:20_000] = 0.01 * ref.synth_iq(20_000, seed=10)
     s[50_000:50_000 + L] += pre
-    s[150_000:150_000 + L] += ratio * pre
+    s[150_000:150_000 + L] += ratio * pre.astype(np.complex128)   # (complex64 * float stays complex64)
     want = ref.find_correlation_peak(*ref.cross_correlate_signals(pre, s, "valid"))
     lag, val, _ = gpu.correlate_peak(pre, s, "valid")
     assert lag == want[0] == (150_000 if ratio > 1 else 50_000)

@@ -142,7 +142,7 @@ def test_correlate_offsets_model():
             np.testing.assert_allclose(model(a, v, mode), np.correlate(a, v, mode), atol=1e-12)
 
 
-def _build_c_example(out):
+def _build_c_example(out, name="chain_c"):
     import shutil
     import subprocess
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -150,13 +150,15 @@ def _build_c_example(out):
     if shutil.which("gcc") is None or not os.path.exists(lib):
         pytest.skip("gcc or libvsig.so missing")
     cmd = ["gcc", "-std=c99", "-O2", "-Wall", "-Werror", "-I", os.path.join(root, "include"),
-           os.path.join(root, "examples", "chain_c.c"), "-L", os.path.dirname(lib), "-lvsig",
-           f"-Wl,-rpath,{os.path.dirname(lib)}", "-lm", "-o", out]
+           os.path.join(root, "examples", name + ".c"), "-L", os.path.dirname(lib), "-lvsig",
+           f"-Wl,-rpath,{os.path.dirname(lib)}", "-lpthread", "-lm", "-o", out]
     subprocess.run(cmd, check=True)
     return out
 
 
-def test_c_example_compiles(tmp_path):
-    """include/vsig.h is plain C99 and examples/chain_c.c links against the
-    library's exported symbols (the non-Python binding of INTEGRATION.md)."""
-    assert os.path.exists(_build_c_example(str(tmp_path / "chain_c")))
+@pytest.mark.parametrize("name", ["chain_c", "shard_c"])
+def test_c_examples_compile(tmp_path, name):
+    """include/vsig.h is plain C99 and the examples (the chain; the sharded
+    chain over the loopback / RCCL transports) link against the library's
+    exported symbols (the non-Python binding of INTEGRATION.md)."""
+    assert os.path.exists(_build_c_example(str(tmp_path / name), name))

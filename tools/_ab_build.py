@@ -1,0 +1,13 @@
+"""Build the A/B libraries next to libvsig.so (same sources, extra defines)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from vector_amd import _build  # noqa: E402
+
+VARIANTS = {
+    "libvsig_x32": ("VSIG_XCORR_BIG_FROM=2049",),
+}
+for name in (sys.argv[1:] or VARIANTS):
+    _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)
+    print("built", name)

@@ -15,8 +15,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvsig.so")
-SOURCES = ["psd.hip", "fir.hip", "xcorr.hip", "reduce.hip", "refine.hip", "analysis.hip", "pfb.hip",
-           "stream_ops.hip", "vsig_api.hip"]
+SOURCES = ["psd.hip", "fir.hip", "xcorr.hip", "reduce.hip", "refine.hip", "bigfft.hip", "analysis.hip", "pfb.hip",
+           "stream_ops.hip", "chain.hip", "vsig_api.hip"]
 HEADERS = ["fft_engine.hpp", "os_common.hpp", "vsig_kernels.h"]
 ARCH = os.environ.get("VSIG_ARCH", "gfx950")
 

@@ -35,6 +35,21 @@ class Peak(C.Structure):
 P = C.c_void_p
 I32, I64, F32 = C.c_int32, C.c_int64, C.c_float
 
+
+class ChainConfig(C.Structure):
+    """vsig_chain_config (include/vsig.h)."""
+    _fields_ = [("n_local", I64), ("taps", P), ("ntaps", I32), ("decim", I32), ("nfft", I32),
+                ("window", P), ("psd_scale", F32), ("tmpl", P), ("L", I64)]
+
+
+SENDRECV = C.CFUNCTYPE(C.c_int, P, P, I64, I32, P, I64, I32, P)
+ALLGATHER = C.CFUNCTYPE(C.c_int, P, P, P, I64, P)
+
+
+class Transport(C.Structure):
+    """vsig_transport (include/vsig.h)."""
+    _fields_ = [("user", P), ("sendrecv", SENDRECV), ("allgather", ALLGATHER)]
+
 # name -> (restype, argtypes); every symbol include/vsig.h declares.
 SIGNATURES = {
     "vsig_version": (C.c_int, []),
@@ -45,6 +60,8 @@ SIGNATURES = {
     "vsig_free": (None, [P]),
     "vsig_last_error": (C.c_char_p, [P]),
     "vsig_set_stream": (C.c_int, [P, P]),
+    "vsig_get_stream": (P, [P]),
+    "vsig_copy_dev": (C.c_int, [P, P, P, I64]),
     "vsig_synchronize": (C.c_int, [P]),
     "vsig_set_option": (C.c_int, [P, C.c_char_p, C.c_int]),
     "vsig_get_option": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_int)]),
@@ -67,6 +84,9 @@ SIGNATURES = {
     "vsig_correlate": (C.c_int, [P, I32, P, I64, P, I64, I32, I32, P, P]),
     "vsig_correlate_c64_dev": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
     "vsig_correlate_c64": (C.c_int, [P, P, I64, P, I64, I32, P, P]),
+    "vsig_dft_dev": (C.c_int, [P, I32, P, I64, I64, I32, I32, P]),
+    "vsig_resample_dev": (C.c_int, [P, I32, P, I64, I64, I32, P]),
+    "vsig_filter_channel_dev": (C.c_int, [P, I32, P, I64, C.c_double, C.c_double, C.c_double, P]),
     "vsig_peak_dev": (C.c_int, [P, I32, P, I64, P]),
     "vsig_peak": (C.c_int, [P, I32, P, I64, P]),
     "vsig_mix_c64_dev": (C.c_int, [P, P, I64, C.c_double, C.c_double, I64, P]),
@@ -82,6 +102,23 @@ SIGNATURES = {
     "vsig_db_dev": (C.c_int, [P, I32, P, I64, C.c_double, P]),
     "vsig_abs_c64_dev": (C.c_int, [P, I32, P, I64, P]),
     "vsig_abs_c128_dev": (C.c_int, [P, I32, P, I64, P]),
+    "vsig_chain_create": (C.c_int, [P, C.POINTER(ChainConfig), I32, I32, C.POINTER(Transport),
+                                    C.POINTER(P)]),
+    "vsig_chain_free": (None, [P]),
+    "vsig_chain_last_error": (C.c_char_p, [P]),
+    "vsig_chain_input": (P, [P]),
+    "vsig_chain_step": (C.c_int, [P]),
+    "vsig_chain_result": (C.c_int, [P, C.POINTER(Peak), C.POINTER(I64)]),
+    "vsig_chain_filtered": (P, [P, C.POINTER(I64)]),
+    "vsig_chain_spectra": (P, [P, C.POINTER(I64)]),
+    "vsig_rccl_available": (C.c_int, []),
+    "vsig_rccl_unique_id": (C.c_int, [C.c_char_p]),
+    "vsig_rccl_comm_init": (C.c_int, [I32, I32, C.c_char_p, I32, C.POINTER(P)]),
+    "vsig_rccl_comm_destroy": (C.c_int, [P]),
+    "vsig_rccl_transport": (C.c_int, [P, C.POINTER(Transport)]),
+    "vsig_loopback_create": (C.c_int, [I32, C.POINTER(P)]),
+    "vsig_loopback_free": (None, [P]),
+    "vsig_loopback_transport": (C.c_int, [P, I32, C.POINTER(Transport)]),
 }
 
 _lib = None

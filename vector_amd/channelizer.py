@@ -1,10 +1,15 @@
-"""Polyphase filter-bank channelizer (BASELINE config 4).
+"""Channel splitting: the reference's own channel filter and the config-4
+polyphase filter-bank channelizer.
 
-No reference counterpart: the reference splits channels with one full-length
-FFT and a brick-wall mask (vector_analyzer/split_channels.py:15-44).  The
-build's definition — a critically sampled windowed-pre-sum PFB — is stated in
-oracle/ref.py (pfb_channelize) and implemented in pfb.hip; parity is against
-that definition only ("parity unpinned" with respect to the reference).
+* ``filter_channel`` -- vector_analyzer/split_channels.py:15-44 as written
+  (one full-length FFT of any length, brick-wall mask, conjugate mirror,
+  inverse FFT, real part), on the any-length transform (bigfft.hip); pinned
+  by tests/golden/channel.npz, made from the reference's function.
+* ``Channelizer`` / ``pfb_channelize`` -- BASELINE config 4's critically
+  sampled windowed-pre-sum PFB (pfb.hip).  It has no reference counterpart;
+  its definition is stated in oracle/ref.py (pfb_channelize) and parity is
+  against that definition only ("parity unpinned" with respect to the
+  reference).
 """
 from __future__ import annotations
 
@@ -14,7 +19,38 @@ import torch
 from . import _lib
 from .dsp import _device_c64, _is_dev, _ptr
 
-__all__ = ["Channelizer", "pfb_channelize"]
+__all__ = ["Channelizer", "pfb_channelize", "filter_channel", "CENTER_FREQ"]
+
+CENTER_FREQ = 5230e6   # vector_analyzer/split_channels.py:7
+
+
+def filter_channel(data, center_freq, sample_rate, bandwidth):
+    """split_channels.filter_channel(data, center_freq, sample_rate, bandwidth):
+    float64 real signal of len(data).  The mask keeps the bins whose
+    ``np.fft.fftfreq(n, 1/sr) * sr + CENTER_FREQ`` (the reference's axis,
+    extra ``* sr`` included) lies within center_freq +- bandwidth/2; the
+    negative half becomes the conjugate mirror of the masked non-negative
+    half.  Odd n > 1 raises ValueError like numpy's shape mismatch does."""
+    ctx = _lib.get_context()
+    dev = _is_dev(data)
+    if dev:
+        t = data.to(torch.complex128 if data.dtype in (torch.complex128, torch.float64)
+                    else torch.complex64).contiguous()
+    else:
+        a = np.asarray(data)
+        wide = a.dtype in (np.complex128, np.float64) or np.issubdtype(a.dtype, np.integer)
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.complex128 if wide else np.complex64)
+                             ).to(f"cuda:{ctx.device}")
+    n = int(t.numel())
+    if n > 1 and n % 2:
+        raise ValueError(f"NumPy boolean array indexing assignment cannot assign {(n + 1) // 2} "
+                         f"input values to the {(n - 1) // 2} output values where the mask is true")
+    y = torch.empty(n, dtype=torch.float64, device=t.device)
+    code = "c128" if t.dtype == torch.complex128 else "c64"
+    ctx.check(ctx.lib.vsig_filter_channel_dev(ctx.h, _lib.DTYPES[code], _ptr(t), n, float(center_freq),
+                                              float(sample_rate), float(bandwidth), _ptr(y)),
+              "filter_channel")
+    return y if dev else y.cpu().numpy()
 
 
 class Channelizer:

@@ -134,8 +134,37 @@ __device__ __forceinline__ long long item_output(const RefineGeom& g, long long 
   return g.rev ? g.nout - 1 - raw : raw;
 }
 
-// Stage 1: one wave per (item, q); lane l one output.  vals / idx / cv are
-// indexed by u * 64 + l, u = item slot * Q + q.
+// Stage 1: one block per (item, q) unit; lane l of every wave one output,
+// the 4 waves a quarter of the taps each (independent partial sums, loads
+// unrolled 8-deep so the loop is throughput- not latency-bound), combined in
+// LDS.  vals / idx / cv are indexed by u * 64 + l, u = item slot * Q + q.
+template <class T>
+__device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __restrict__ v,
+                                           long long abase, long long k0, long long k1,
+                                           double& re, double& im) {
+  long long k = k0;
+  double r0 = 0, r1 = 0, i0 = 0, i1 = 0;
+  for (; k + 8 <= k1; k += 8) {
+    double2 x[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) { x[j] = ld2<T>(a, abase + k + j); y[j] = ld2<T>(v, k + j); }
+#pragma unroll
+    for (int j = 0; j < 8; j += 2) {
+      r0 = fma(x[j].x, y[j].x, r0); r0 = fma(x[j].y, y[j].y, r0);
+      i0 = fma(x[j].y, y[j].x, i0); i0 = fma(-x[j].x, y[j].y, i0);
+      r1 = fma(x[j + 1].x, y[j + 1].x, r1); r1 = fma(x[j + 1].y, y[j + 1].y, r1);
+      i1 = fma(x[j + 1].y, y[j + 1].x, i1); i1 = fma(-x[j + 1].x, y[j + 1].y, i1);
+    }
+  }
+  for (; k < k1; ++k) {
+    const double2 x = ld2<T>(a, abase + k), y = ld2<T>(v, k);
+    r0 = fma(x.x, y.x, r0); r0 = fma(x.y, y.y, r0);
+    i0 = fma(x.y, y.x, i0); i0 = fma(-x.x, y.y, i0);
+  }
+  re = r0 + r1;
+  im = i0 + i1;
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void refine_stage1(const T* __restrict__ a, const T* __restrict__ v,
                                                      RefineGeom g, const long long* __restrict__ items,
@@ -146,45 +175,56 @@ __global__ __launch_bounds__(256) void refine_stage1(const T* __restrict__ a, co
   const long long cnt = (long long)keys->count;
   if (keys->status || cnt == 0) return;
   const long long nunits = (cnt < cap ? cnt : cap) * g.Q;
-  const int l = threadIdx.x & 63;
-  const long long wave0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long u = wave0; u < nunits; u += nwaves) {
+  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __shared__ double pr[4][64], pi[4][64];
+  for (long long u = blockIdx.x; u < nunits; u += gridDim.x) {   // uniform per block
     const long long item = items[u / g.Q];
     const int q = (int)(u % g.Q);
     const long long o = item_output(g, item, q, l);
-    double re = 0.0, im = 0.0, m2 = -1.0;
+    double re = 0.0, im = 0.0;
     if (o >= 0) {
       const long long i = g.F + o;
       long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
-      const long long abase = i - (g.nv - 1);
-      for (long long k = k0; k < k1; ++k) {
-        const double2 x = ld2<T>(a, abase + k);
-        const double2 y = ld2<T>(v, k);
-        re = fma(x.x, y.x, re);          // x * conj(y)
-        re = fma(x.y, y.y, re);
-        im = fma(x.y, y.x, im);
-        im = fma(-x.x, y.y, im);
-      }
-      m2 = re * re + im * im;
+      const long long span = (k1 - k0 + 3) / 4;          // this wave's quarter of the taps
+      const long long q0 = k0 + w * span;
+      const long long q1 = q0 + span < k1 ? q0 + span : k1;
+      if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im);
     }
-    const long long e = u * 64 + l;
-    vals[e] = m2;
-    oidx[e] = o;
-    cv[e] = make_double2(re, im);
-    double wm = m2;
+    pr[w][l] = re;
+    pi[w][l] = im;
+    __syncthreads();
+    if (w == 0) {
+      re = (pr[0][l] + pr[1][l]) + (pr[2][l] + pr[3][l]);
+      im = (pi[0][l] + pi[1][l]) + (pi[2][l] + pi[3][l]);
+      const double m2 = o >= 0 ? re * re + im * im : -1.0;
+      const long long e = u * 64 + l;
+      vals[e] = m2;
+      oidx[e] = o;
+      cv[e] = make_double2(re, im);
+      double wm = m2;
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      const double o2 = __shfl_xor(wm, off);
-      wm = o2 > wm ? o2 : wm;
+      for (int off = 32; off > 0; off >>= 1) {
+        const double o2 = __shfl_xor(wm, off);
+        wm = o2 > wm ? o2 : wm;
+      }
+      if (l == 0 && wm >= 0.0) atomicMax(&keys->max1, (unsigned long long)__double_as_longlong(wm));
     }
-    if (l == 0 && wm >= 0.0) atomicMax(&keys->max1, (unsigned long long)__double_as_longlong(wm));
+    __syncthreads();
   }
 }
 
-// Stage 2: compensated recomputation of the outputs within eps2 of the stage-1
-// max; the others drop out (vals = -1).
+// Stage 2: the outputs within eps2 of the stage-1 max recomputed by a
+// compensated dot product, one wave per output (lane l takes taps k = l mod
+// 64: Dot2 partials (s, c) per lane, combined across lanes by TwoSum, which
+// keeps Dot2's bound); the others drop out (vals = -1).
+__device__ __forceinline__ void two_sum_pair(double& s, double& c, double s2, double c2) {
+  double t, e;
+  two_sum(s, s2, t, e);
+  s = t;
+  c = c + c2 + e;
+}
+
 template <class T>
 __global__ __launch_bounds__(256) void refine_stage2(const T* __restrict__ a, const T* __restrict__ v,
                                                      RefineGeom g, long long cap, double eps2,
@@ -197,29 +237,45 @@ __global__ __launch_bounds__(256) void refine_stage2(const T* __restrict__ a, co
   const long long n = (cnt < cap ? cnt : cap) * g.Q * 64;
   const double m1 = __longlong_as_double((long long)keys->max1);
   const double thr = m1 * (1.0 - eps2);
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-    const double v1 = vals[e];
-    if (v1 < 0.0) continue;
-    if (v1 < thr) { vals[e] = -1.0; continue; }
-    const long long i = g.F + oidx[e];
-    long long k0, k1;
-    tap_range(i, g.na, g.nv, k0, k1);
-    const long long abase = i - (g.nv - 1);
-    double sr = 0.0, cr = 0.0, si = 0.0, ci = 0.0;
-    for (long long k = k0; k < k1; ++k) {
-      const double2 x = ld2<T>(a, abase + k);
-      const double2 y = ld2<T>(v, k);
-      dot2_add(sr, cr, x.x, y.x);
-      dot2_add(sr, cr, x.y, y.y);
-      dot2_add(si, ci, x.y, y.x);
-      dot2_add(si, ci, -x.x, y.y);
+  const int l = threadIdx.x & 63;
+  const long long wave0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long base = wave0 * 64; base < n; base += nwaves * 64) {   // 64 entries per wave
+    const long long e = base + l;
+    const double v1 = e < n ? vals[e] : -1.0;
+    const bool surv = v1 >= 0.0 && v1 >= thr;
+    if (e < n && v1 >= 0.0 && !surv) vals[e] = -1.0;
+    unsigned long long mask = __ballot(surv);
+    while (mask) {
+      const int src = __builtin_ctzll(mask);
+      mask &= mask - 1;
+      const long long es = base + src;
+      const long long i = g.F + oidx[es];                 // uniform
+      long long k0, k1;
+      tap_range(i, g.na, g.nv, k0, k1);
+      const long long abase = i - (g.nv - 1);
+      double sr = 0.0, cr = 0.0, si = 0.0, ci = 0.0;
+      for (long long k = k0 + l; k < k1; k += 64) {
+        const double2 x = ld2<T>(a, abase + k);
+        const double2 y = ld2<T>(v, k);
+        dot2_add(sr, cr, x.x, y.x);
+        dot2_add(sr, cr, x.y, y.y);
+        dot2_add(si, ci, x.y, y.x);
+        dot2_add(si, ci, -x.x, y.y);
+      }
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        two_sum_pair(sr, cr, __shfl_xor(sr, off), __shfl_xor(cr, off));
+        two_sum_pair(si, ci, __shfl_xor(si, off), __shfl_xor(ci, off));
+      }
+      if (l == 0) {
+        const double re = sr + cr, im = si + ci;
+        const double m2 = re * re + im * im;
+        vals[es] = m2;
+        cv[es] = make_double2(re, im);
+        atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(m2));
+      }
     }
-    const double re = sr + cr, im = si + ci;
-    const double m2 = re * re + im * im;
-    vals[e] = m2;
-    cv[e] = make_double2(re, im);
-    atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(m2));
   }
 }
 
@@ -287,10 +343,11 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
     hipLaunchKernelGGL(refine_select_partials, dim3((unsigned)grid), dim3(256), 0, st, r.parts,
                        r.nparts, rec, r.eps, r.cap_items, items, keys);
   }
-  // stage grids: enough waves for the cap, at most 4 x 256 CUs x 8 waves
-  long long waves = r.cap_items * r.Q;
-  if (waves > 8192) waves = 8192;
-  const unsigned g1 = (unsigned)((waves + 3) / 4);
+  // stage grids: stage 1 one block per unit (grid-stride), stage 2 one wave
+  // per 64 entries (grid-stride), capped at a few blocks per CU
+  long long units = r.cap_items * r.Q;
+  if (units > 4096) units = 4096;
+  const unsigned g1 = (unsigned)units;
   long long g2l = (n + 255) / 256;
   if (g2l > 4096) g2l = 4096;
   const unsigned g2 = (unsigned)g2l;

@@ -35,6 +35,12 @@ struct vsig_ctx {
   int refine_eps_ppm = 1000;             // fp32 candidate band (relative, ppm of max |c|)
   long long refine_cap = 1LL << 20;      // max outputs revisited (else record left fp32)
   bool refine_ran = false;
+  struct Chirp { long long M; float2* c; float2* B; };
+  std::map<long long, Chirp> chirps;     // Bluestein plans by length (bigfft.hip)
+  void* bigtmp = nullptr;                // four-step scratch
+  size_t bigtmp_bytes = 0;
+  void* spec[2] = {nullptr, nullptr};    // resample / channel spectra
+  size_t spec_bytes[2] = {0, 0};
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
@@ -200,10 +206,14 @@ int os_size_fir(int ntaps) {
   if (ntaps <= 8192) return 16384;
   return 0;
 }
+#ifndef VSIG_XCORR_BIG_FROM
+#define VSIG_XCORR_BIG_FROM 8193     // templates from this length use M = 32768
+#endif
 int os_size_xcorr(long long L) {
   if (L <= 1024) return 4096;
   if (L <= 2048) return 8192;
-  if (L <= 8192) return 16384;
+  if (L < VSIG_XCORR_BIG_FROM && L <= 8192) return 16384;
+  if (L <= 16384) return 32768;
   return 0;
 }
 
@@ -217,13 +227,21 @@ int ensure_buf(vsig_ctx* c, void** buf, size_t* have, size_t bytes) {
   return VSIG_OK;
 }
 
-// FFT_M(zero-padded u[0..len)) * gain into a new device buffer.
+// FFT_M(zero-padded u[0..len)) / M into a new device buffer (natural order;
+// M > 16384 by the four-step passes of bigfft.hip).
+int big_plan_fwd(vsig_ctx* c, long long M, const float2* u, long long len, float2* S);
 int make_spectrum(vsig_ctx* c, const float2* u_dev, int len, int M, float2** out) {
-  const float2* tw;
-  int rc = get_twiddles(c, M, &tw);
-  if (rc) return rc;
   float2* S = nullptr;
   HIPCHK(c, hipMalloc(&S, (size_t)M * sizeof(float2)));
+  if (M > 16384) {
+    const int rc = big_plan_fwd(c, M, u_dev, len, S);
+    if (rc) { (void)hipFree(S); return rc; }
+    *out = S;
+    return VSIG_OK;
+  }
+  const float2* tw;
+  int rc = get_twiddles(c, M, &tw);
+  if (rc) { (void)hipFree(S); return rc; }
   hipError_t e = vsig::launch_spectrum_prep(M, u_dev, len, 1.0f / (float)M, S, tw, c->stream);
   if (e != hipSuccess) { (void)hipFree(S); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
   *out = S;
@@ -277,6 +295,147 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
   Timed t(c, "refine");
   HIPCHK(c, vsig::launch_refine(r, c->stream));
   c->refine_ran = true;
+  return VSIG_OK;
+}
+
+// W_M^m for the four-step twiddles (bigfft.hip): two-level table
+// A[i] = W_M^(i 2^S), B[j] = W_M^j, S = ceil(log2 M / 2), built in double.
+int get_tw_big(vsig_ctx* c, long long M, const float2** out, int* S, int* hiA) {
+  int lg = 0;
+  while ((1LL << lg) < M) ++lg;
+  *S = (lg + 1) / 2;
+  *hiA = (int)(M >> *S);
+  const int key = (1 << 22) + lg;
+  auto it = c->tw.find(key);
+  if (it != c->tw.end()) { *out = it->second; return VSIG_OK; }
+  std::vector<float2> h;
+  for (long long i = 0; i < *hiA; ++i) {
+    const double a = -2.0 * M_PI * (double)(i << *S) / (double)M;
+    h.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+  }
+  for (long long j = 0; j < (1LL << *S); ++j) {
+    const double a = -2.0 * M_PI * (double)j / (double)M;
+    h.push_back(make_float2((float)std::cos(a), (float)std::sin(a)));
+  }
+  float2* d = nullptr;
+  HIPCHK(c, hipMalloc(&d, h.size() * sizeof(float2)));
+  HIPCHK(c, hipMemcpy(d, h.data(), h.size() * sizeof(float2), hipMemcpyHostToDevice));
+  c->tw[key] = d;
+  *out = d;
+  return VSIG_OK;
+}
+
+constexpr long long kBigMax = 1LL << 28;    // largest four-step transform
+
+// split_channels.py's frequency axis, as numpy forms it: fftfreq(n, 1/sr)[k]
+// * sr + CENTER_FREQ (k >= 0 here, or -1), no contraction into FMAs.
+#pragma clang fp contract(off)
+double channel_freq(long long k, long long n, double sr, double center) {
+  const double d = 1.0 / sr;
+  const double val = 1.0 / ((double)n * d);
+  const double f = (double)k * val;
+  const double g = f * sr;
+  return g + center;
+}
+#pragma clang fp contract(on)
+
+// Twiddles of a (four-step) transform of M points.
+struct BigPlan {
+  long long M;
+  int N1, N2, S, hiA;
+  const float2 *tw1, *tw2, *t2;
+};
+int big_plan(vsig_ctx* c, long long M, BigPlan* p) {
+  p->M = M;
+  vsig::bigfft_split(M, &p->N1, &p->N2);
+  int rc;
+  p->tw1 = p->t2 = nullptr;
+  p->S = p->hiA = 0;
+  if ((rc = get_twiddles(c, p->N2, &p->tw2))) return rc;
+  if (p->N1 > 1) {
+    if ((rc = get_twiddles(c, p->N1, &p->tw1))) return rc;
+    if ((rc = get_tw_big(c, M, &p->t2, &p->S, &p->hiA))) return rc;
+  }
+  return VSIG_OK;
+}
+
+// S = FFT_M(zero-padded u[0..len)) / M in natural order (four-step, M > 16384).
+int big_plan_fwd(vsig_ctx* c, long long M, const float2* u, long long len, float2* S) {
+  BigPlan bp;
+  int rc = big_plan(c, M, &bp);
+  if (rc) return rc;
+  if ((rc = ensure_buf(c, &c->bigtmp, &c->bigtmp_bytes, (size_t)M * sizeof(float2)))) return rc;
+  vsig::BigIn in{u, 0, 0, 1, len, nullptr, nullptr, 0, 1.0f / (float)M};
+  HIPCHK(c, vsig::launch_bf_col(bp.N1, bp.N2, 1, in, (float2*)c->bigtmp, bp.tw1, bp.t2, bp.S, bp.hiA,
+                                c->stream));
+  HIPCHK(c, vsig::launch_bf_row(3, bp.N1, bp.N2, 1, (float2*)c->bigtmp, nullptr, bp.tw2, 1.0f,
+                                reinterpret_cast<float*>(S), 0, c->stream));
+  return VSIG_OK;
+}
+
+// Bluestein plan for length N: chirp c[N] and B = FFT_M(b) / M (permuted order
+// for the four-step sizes), M = the power of two >= max(256, 2N - 1).
+int chirp_plan(vsig_ctx* c, long long N, vsig_ctx::Chirp** out) {
+  auto it = c->chirps.find(N);
+  if (it != c->chirps.end()) { *out = &it->second; return VSIG_OK; }
+  long long M = 256;
+  while (M < 2 * N - 1) M *= 2;
+  if (M > kBigMax) return fail(c, VSIG_E_UNSUPPORTED, "transform length above 2^27");
+  BigPlan bp;
+  int rc = big_plan(c, M, &bp);
+  if (rc) return rc;
+  float2 *cv = nullptr, *B = nullptr, *b = nullptr;
+  auto cleanup = [&]() { if (cv) (void)hipFree(cv); if (B) (void)hipFree(B); if (b) (void)hipFree(b); };
+  if (hipMalloc(&cv, N * sizeof(float2)) != hipSuccess || hipMalloc(&B, M * sizeof(float2)) != hipSuccess ||
+      hipMalloc(&b, M * sizeof(float2)) != hipSuccess) {
+    cleanup();
+    return fail(c, VSIG_E_NOMEM, "Bluestein plan allocation");
+  }
+  hipError_t e = vsig::launch_bf_chirp(N, M, cv, b, c->stream);
+  vsig::BigIn in{b, 0, 0, 1, M, nullptr, nullptr, 0, 1.0f / (float)M};
+  if (e == hipSuccess) {
+    if (bp.N1 == 1) {
+      vsig::BigOut o{B, 0, 0, M, nullptr, 0, 1.0f};
+      e = vsig::launch_bf_small(1, (int)M, 1, in, o, nullptr, bp.tw2, c->stream);
+    } else {
+      e = vsig::launch_bf_col(bp.N1, bp.N2, 1, in, B, bp.tw1, bp.t2, bp.S, bp.hiA, c->stream);
+      if (e == hipSuccess)
+        e = vsig::launch_bf_row(1, bp.N1, bp.N2, 1, B, nullptr, bp.tw2, 1.0f, nullptr, 0, c->stream);
+    }
+  }
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(b);
+  b = nullptr;
+  if (e != hipSuccess) { cleanup(); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
+  auto& ch = c->chirps[N];
+  ch = vsig_ctx::Chirp{M, cv, B};
+  *out = &ch;
+  return VSIG_OK;
+}
+
+// DFT of any length N (batch frames): X[k] = sum_n x[n] W_N^(nk), or the
+// inverse (conj) form; in / out describe the operands (their chirp / conj
+// fields are set here), out.scale includes any 1/N.
+int dft_any(vsig_ctx* c, long long N, long long batch, vsig::BigIn in, vsig::BigOut out, bool inverse) {
+  vsig_ctx::Chirp* ch;
+  int rc = chirp_plan(c, N, &ch);
+  if (rc) return rc;
+  BigPlan bp;
+  if ((rc = big_plan(c, ch->M, &bp))) return rc;
+  in.chirp = ch->c;
+  in.conj = inverse ? 1 : 0;
+  in.nvalid = in.nvalid < N ? in.nvalid : N;
+  out.chirp = ch->c;
+  out.conj = inverse ? 1 : 0;
+  if (bp.N1 == 1) {
+    HIPCHK(c, vsig::launch_bf_small(0, (int)ch->M, batch, in, out, ch->B, bp.tw2, c->stream));
+    return VSIG_OK;
+  }
+  if ((rc = ensure_buf(c, &c->bigtmp, &c->bigtmp_bytes, (size_t)(batch * ch->M) * sizeof(float2)))) return rc;
+  float2* tmp = static_cast<float2*>(c->bigtmp);
+  HIPCHK(c, vsig::launch_bf_col(bp.N1, bp.N2, batch, in, tmp, bp.tw1, bp.t2, bp.S, bp.hiA, c->stream));
+  HIPCHK(c, vsig::launch_bf_row(0, bp.N1, bp.N2, batch, tmp, ch->B, bp.tw2, 1.0f, nullptr, 0, c->stream));
+  HIPCHK(c, vsig::launch_bf_icol(bp.N1, bp.N2, batch, tmp, out, bp.tw1, bp.t2, bp.S, bp.hiA, c->stream));
   return VSIG_OK;
 }
 
@@ -337,11 +496,16 @@ void vsig_free(vsig_ctx* c) {
   for (int i = 0; i < 3; ++i) if (c->stage[i]) (void)hipFree(c->stage[i]);
   for (int i = 0; i < 3; ++i) if (c->conv[i]) (void)hipFree(c->conv[i]);
   if (c->rscratch) (void)hipFree(c->rscratch);
+  for (auto& kv : c->chirps) { (void)hipFree(kv.second.c); (void)hipFree(kv.second.B); }
+  if (c->bigtmp) (void)hipFree(c->bigtmp);
+  for (int i = 0; i < 2; ++i) if (c->spec[i]) (void)hipFree(c->spec[i]);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
 
 const char* vsig_last_error(const vsig_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+void* vsig_get_stream(vsig_ctx* c) { return c ? (void*)c->stream : nullptr; }
 
 int vsig_set_stream(vsig_ctx* c, void* s) {
   if (!c) return VSIG_E_INVALID;
@@ -408,6 +572,12 @@ int vsig_copy_bench(vsig_ctx* c, const void* x, int64_t n, void* y, int variant,
 }
 #endif
 
+int vsig_copy_dev(vsig_ctx* c, void* dst, const void* src, int64_t bytes) {
+  if (!c || !dst || !src || bytes < 0) return fail(c, VSIG_E_INVALID, "bad copy");
+  if (bytes) HIPCHK(c, hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDefault, c->stream));
+  return VSIG_OK;
+}
+
 int vsig_synchronize(vsig_ctx* c) {
   if (!c) return VSIG_E_INVALID;
   HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -442,11 +612,31 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
                      float* sxx, int64_t nframes) {
   if (!c || !x || !win || !sxx) return fail(c, VSIG_E_INVALID, "null pointer");
   if (stride < 1) return fail(c, VSIG_E_INVALID, "stride must be >= 1");
-  if (!pow2_in(nfft, 64, 16384))
-    return fail(c, VSIG_E_UNSUPPORTED, "nfft must be a power of two in [64, 16384]");
+  if (!pow2_in(nfft, 64, kBigMax))
+    return fail(c, VSIG_E_UNSUPPORTED, "nfft must be a power of two in [64, 2^28]");
   if (nperseg < 1 || nperseg > nfft || hop < 1 || n < nperseg)
     return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
+  if (nfft > 16384) {          // long frames: four-step FFT per frame (bigfft.hip)
+    BigPlan bp;
+    int rc = big_plan(c, nfft, &bp);
+    if (rc) return rc;
+    long long fb = (256LL << 20) / ((long long)nfft * 8);   // frames per 256 MB of scratch
+    if (fb < 1) fb = 1;
+    if (fb > nframes) fb = nframes;
+    if ((rc = ensure_buf(c, &c->bigtmp, &c->bigtmp_bytes, (size_t)(fb * nfft) * sizeof(float2)))) return rc;
+    Timed t(c, "psd");
+    for (long long f0 = 0; f0 < nframes; f0 += fb) {
+      const long long nb = nframes - f0 < fb ? nframes - f0 : fb;
+      vsig::BigIn in{(const float2*)x + f0 * hop * stride, 0, hop * stride, stride, nperseg, nullptr,
+                     win, 0, 1.0f};
+      HIPCHK(c, vsig::launch_bf_col(bp.N1, bp.N2, nb, in, (float2*)c->bigtmp, bp.tw1, bp.t2, bp.S,
+                                    bp.hiA, c->stream));
+      HIPCHK(c, vsig::launch_bf_row(2, bp.N1, bp.N2, nb, (float2*)c->bigtmp, nullptr, bp.tw2, scale,
+                                    sxx + f0 * nfft, shift, c->stream));
+    }
+    return VSIG_OK;
+  }
   const float2* tw;
   // pair kernel (>= 256 threads per frame): per-pass table; smaller plans: two-level table
   const bool pair = vsig::psd_plan_threads(nfft) >= 256;
@@ -599,14 +789,15 @@ static int xcorr_build(vsig_ctx* c, const float2* td, long long L, vsig_xcorr* x
   constexpr long long B = 8192;
   x->ctx = c;
   x->L = L;
-  x->M = L <= B ? os_size_xcorr(L) : 16384;
-  for (long long p = 0; p * B < L || p == 0; ++p) {
-    const long long Lp = L <= B ? L : ((L - p * B) < B ? (L - p * B) : B);
+  x->M = os_size_xcorr(L) ? os_size_xcorr(L) : 16384;
+  const long long Bc = x->M == 32768 ? 16384 : B;    // one pass up to 16384 at M = 32768
+  for (long long p = 0; p * Bc < L || p == 0; ++p) {
+    const long long Lp = L <= Bc ? L : ((L - p * Bc) < B ? (L - p * Bc) : B);
     float2* P = nullptr;
     const int rc = make_spectrum(c, td + p * B, (int)Lp, x->M, &P);
     if (rc) return rc;
     x->Ps.push_back(P);
-    if (L <= B) break;
+    if (L <= Bc) break;
   }
   return VSIG_OK;
 }
@@ -633,7 +824,7 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
                      const RefineOperands* op, void* out128) {
   vsig_ctx* c = x->ctx;
   PeakPartial* rec = peak_dev ? reinterpret_cast<PeakPartial*>(peak_dev) : c->result;
-  if (x->Ps.size() == 1 && x->L <= 8192) {
+  if (x->Ps.size() == 1 && x->L <= (x->M == 32768 ? 16384 : 8192)) {
     const long long hop = (long long)x->M - x->L + 1;
     const long long nblocks = (nout + hop - 1) / hop;
     int waves, Q, stride, plan;
@@ -645,7 +836,7 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     const float2* tw;
     const float2* wt = nullptr;
     if ((rc = get_twiddles(c, plan, &tw))) return rc;
-    if (x->M == 16384 && (rc = get_half_tw(c, x->M, 256, &wt))) return rc;
+    if (x->M >= 16384 && (rc = get_half_tw(c, x->M, x->M == 16384 ? 256 : 1024, &wt))) return rc;
     {
       Timed t(c, "xcorr");
       HIPCHK(c, vsig::launch_xcorr_os(x->M, s, n, x->Ps[0], off, nout, hop, cout, store_mode,
@@ -822,6 +1013,101 @@ int vsig_correlate(vsig_ctx* c, int32_t dtype, const void* a, int64_t na, const 
 int vsig_correlate_c64(vsig_ctx* c, const void* a, int64_t na, const void* v, int64_t nv,
                        int32_t mode, void* cout, vsig_peak_t* peak) {
   return vsig_correlate(c, VSIG_DTYPE_C64, a, na, v, nv, mode, VSIG_DTYPE_C64, cout, peak);
+}
+
+// ---------------------------------------------------------------- any-length transforms
+int vsig_dft_dev(vsig_ctx* c, int32_t dtype, const void* x, int64_t n, int64_t batch, int32_t inverse,
+                 int32_t out_dtype, void* y) {
+  if (!c || !x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1 || batch < 1) return fail(c, VSIG_E_INVALID, "need n >= 1 and batch >= 1");
+  if ((dtype != VSIG_DTYPE_C64 && dtype != VSIG_DTYPE_C128) ||
+      (out_dtype != VSIG_DTYPE_C64 && out_dtype != VSIG_DTYPE_C128))
+    return fail(c, VSIG_E_INVALID, "dtype must be VSIG_DTYPE_C64 or VSIG_DTYPE_C128");
+  vsig::BigIn in{x, dtype == VSIG_DTYPE_C128 ? 1 : 0, n, 1, n, nullptr, nullptr, 0, 1.0f};
+  vsig::BigOut out{y, out_dtype == VSIG_DTYPE_C128 ? 1 : 0, n, n, nullptr, 0,
+                   inverse ? (float)(1.0 / (double)n) : 1.0f};
+  Timed t(c, "dft");
+  return dft_any(c, n, batch, in, out, inverse != 0);
+}
+
+int vsig_resample_dev(vsig_ctx* c, int32_t dtype, const void* x, int64_t n, int64_t num,
+                      int32_t real_input, void* y) {
+  if (!c || !x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1 || num < 1) return fail(c, VSIG_E_INVALID, "need n >= 1 and num >= 1");
+  if (dtype != VSIG_DTYPE_C64 && dtype != VSIG_DTYPE_C128)
+    return fail(c, VSIG_E_INVALID, "dtype must be VSIG_DTYPE_C64 or VSIG_DTYPE_C128");
+  int rc;
+  if ((rc = ensure_buf(c, &c->spec[0], &c->spec_bytes[0], (size_t)n * 8)) ||
+      (rc = ensure_buf(c, &c->spec[1], &c->spec_bytes[1], (size_t)num * 8)))
+    return rc;
+  float2* X = (float2*)c->spec[0];
+  float2* Y = (float2*)c->spec[1];
+  Timed t(c, "resample");
+  vsig::BigIn in{x, dtype == VSIG_DTYPE_C128 ? 1 : 0, n, 1, n, nullptr, nullptr, 0, 1.0f};
+  vsig::BigOut ox{X, 0, n, n, nullptr, 0, 1.0f};
+  if ((rc = dft_any(c, n, 1, in, ox, false))) return rc;
+  HIPCHK(c, vsig::launch_resample_spectrum(X, n, num, Y, c->stream));
+  // y = ifft(Y) * num / n  ->  the inverse DFT's 1/num and num/n leave 1/n
+  vsig::BigIn iy{Y, 0, num, 1, num, nullptr, nullptr, 0, 1.0f};
+  vsig::BigOut oy{y, real_input ? 3 : 0, num, num, nullptr, 0, (float)(1.0 / (double)n)};
+  return dft_any(c, num, 1, iy, oy, true);
+}
+
+int vsig_filter_channel_dev(vsig_ctx* c, int32_t dtype, const void* x, int64_t n,
+                            double center_freq, double sample_rate, double bandwidth,
+                            double* y) {
+  if (!c || !x || !y) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  if (n > 1 && (n & 1))
+    return fail(c, VSIG_E_INVALID, "odd length: the conjugate mirror's halves differ (numpy "
+                                   "raises on the shape mismatch)");
+  if (dtype != VSIG_DTYPE_C64 && dtype != VSIG_DTYPE_C128)
+    return fail(c, VSIG_E_INVALID, "dtype must be VSIG_DTYPE_C64 or VSIG_DTYPE_C128");
+  const double center = 5230e6;                  // split_channels.py:7 CENTER_FREQ
+  const double lo = center_freq - bandwidth / 2, hi = center_freq + bandwidth / 2;
+  if (n > 1) {   // the mirror's halves are the natural ones unless f(-1) rounds onto CENTER
+    if (!(channel_freq(-1, n, sample_rate, center) < center))
+      return fail(c, VSIG_E_UNSUPPORTED, "frequency spacing below the rounding of CENTER_FREQ");
+  }
+  // kept non-negative bins: f(k) rises with k, so the mask is one range [ka, kb]
+  const long long h = n == 1 ? 1 : n / 2;
+  auto keep = [&](long long k) { const double f = channel_freq(k, n, sample_rate, center); return f >= lo && f <= hi; };
+  auto first_at_least = [&](double bound) {      // smallest k in [0, h] with f(k) >= bound
+    long long a = 0, b = h;
+    while (a < b) { const long long m = (a + b) / 2; if (channel_freq(m, n, sample_rate, center) >= bound) b = m; else a = m + 1; }
+    return a;
+  };
+  long long ka = first_at_least(lo), kb = ka - 1;
+  if (ka < h && keep(ka)) {
+    long long a = ka, b = h - 1;                 // largest kept k
+    while (a < b) { const long long m = (a + b + 1) / 2; if (keep(m)) a = m; else b = m - 1; }
+    kb = a;
+  }
+  const long long nk = kb >= ka ? kb - ka + 1 : 0;
+  int rc;
+  if (nk * n <= (1LL << 32)) {                   // direct double-precision path
+    if ((rc = ensure_buf(c, &c->spec[0], &c->spec_bytes[0], (size_t)(nk > 0 ? nk : 1) * 256 * 16)) ||
+        (rc = ensure_buf(c, &c->spec[1], &c->spec_bytes[1], (size_t)(nk > 0 ? nk : 1) * 16)))
+      return rc;
+    Timed t(c, "channel");
+    HIPCHK(c, vsig::launch_channel_direct(dtype == VSIG_DTYPE_C128, x, n, ka, kb, (double2*)c->spec[0],
+                                          (double2*)c->spec[1], y, c->stream));
+    return VSIG_OK;
+  }
+  if ((rc = ensure_buf(c, &c->spec[0], &c->spec_bytes[0], (size_t)n * 8)) ||
+      (rc = ensure_buf(c, &c->spec[1], &c->spec_bytes[1], (size_t)n * 8)))
+    return rc;
+  float2* X = (float2*)c->spec[0];
+  float2* F = (float2*)c->spec[1];
+  Timed t(c, "channel");
+  vsig::BigIn in{x, dtype == VSIG_DTYPE_C128 ? 1 : 0, n, 1, n, nullptr, nullptr, 0, 1.0f};
+  vsig::BigOut ox{X, 0, n, n, nullptr, 0, 1.0f};
+  if ((rc = dft_any(c, n, 1, in, ox, false))) return rc;
+  HIPCHK(c, vsig::launch_channel_mask(X, n, sample_rate, center, center_freq - bandwidth / 2,
+                                      center_freq + bandwidth / 2, F, c->stream));
+  vsig::BigIn iF{F, 0, n, 1, n, nullptr, nullptr, 0, 1.0f};
+  vsig::BigOut oy{y, 2, n, n, nullptr, 0, (float)(1.0 / (double)n)};
+  return dft_any(c, n, 1, iF, oy, true);
 }
 
 // ---------------------------------------------------------------- peak

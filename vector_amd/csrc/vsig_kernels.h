@@ -151,6 +151,44 @@ size_t refine_scratch_bytes(long long cap_items, int Q);
 hipError_t launch_refine(const RefineArgs& r, hipStream_t st);
 hipError_t launch_convert_c(int to128, const void* x, long long n, void* y, hipStream_t st);
 
+// bigfft.hip: four-step FFT of M = N1 N2 > 16384 points, Bluestein for any
+// length (see the file's header).
+struct BigIn {                 // operand n of frame f
+  const void* src;
+  int kind;                    // 0 complex64, 1 complex128, 2 zeros
+  long long fstride, estride, nvalid;
+  const float2* chirp;         // optional * chirp[n]
+  const float* win;            // optional * win[n]
+  int conj;                    // conj(x) first (inverse DFT)
+  float scale;
+};
+struct BigOut {                // natural-order result n of frame f
+  void* dst;
+  int kind;                    // 0 complex64, 1 complex128, 2 float64 real part, 3 complex64 real part
+  long long fstride, nout;
+  const float2* chirp;         // optional * chirp[n], then conj
+  int conj;
+  float scale;
+};
+void bigfft_split(long long M, int* N1, int* N2);
+hipError_t launch_bf_chirp(long long N, long long M, float2* c, float2* b, hipStream_t st);
+hipError_t launch_bf_col(int N1, int N2, long long batch, const BigIn& in, float2* tmp,
+                         const float2* tw1, const float2* t2, int S, int hiA, hipStream_t st);
+hipError_t launch_bf_icol(int N1, int N2, long long batch, float2* tmp, const BigOut& out,
+                          const float2* tw1, const float2* t2, int S, int hiA, hipStream_t st);
+hipError_t launch_bf_row(int mode, int N1, int N2, long long batch, float2* tmp, const float2* Bk,
+                         const float2* tw2, float scale, float* psd, int shift, hipStream_t st);
+hipError_t launch_bf_small(int mode, int M, long long batch, const BigIn& in, const BigOut& out,
+                           const float2* Bk, const float2* tw, hipStream_t st);
+hipError_t launch_resample_spectrum(const float2* X, long long Nx, long long num, float2* Y,
+                                    hipStream_t st);
+hipError_t launch_channel_mask(const float2* X, long long n, double sr, double center, double lo,
+                               double hi, float2* F, hipStream_t st);
+// kept bins [ka, kb] (kb < ka: none) of the channel filter by direct double sums;
+// part: 256 * (kb - ka + 1) scratch, X: kb - ka + 1
+hipError_t launch_channel_direct(int c128, const void* x, long long n, long long ka, long long kb,
+                                 double2* part, double2* X, double* y, hipStream_t st);
+
 // pfb.hip: C in {64, 128, 256}, PT in {4, 8, 16}; y frame-major (M x C)
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,
                       float2* y, const float2* tw, hipStream_t st);

@@ -2,6 +2,7 @@
 // |c|^2 argmax / sums epilogue (correlate, find_correlation_peak).
 //   M = 16384 (templates of 2049 .. 8192 samples): xcorr_half_kernel, two
 //     8192-point halves through LDS, two blocks per CU;
+//   M = 32768 (8193 .. 16384): the same with 16384-point halves;
 //   M = 4096 / 8192 (templates up to 1024 / 2048): xcorr_os_kernel, one frame
 //     per block, persistent with the next segment prefetched.
 // Both use register twiddle anchors (no global loads inside a transform).
@@ -117,6 +118,13 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
 // so W_M^j = W_M^t * W_64^K(e): one per-thread twiddle (table wt) and a
 // compile-time 64th root per element.
 // ---------------------------------------------------------------------------
+// The M = 32768 correlator (templates of 8193 .. 16384 samples in one pass):
+// 16384-point halves, 512 threads x 32 values, 3 passes, one block per CU.
+// Measured on templates of 4096 (VSIG_XCORR_BIG_FROM=2049 builds): 1.89 ms
+// per 2^28 samples against 1.42 ms for the M = 16384 kernel (r02_v6 A/B), so
+// shorter templates keep M = 16384.
+using PlanX32k = Plan16384w;
+
 template <class P, int M>
 constexpr int half_root(int e) {
   return ((e / P::R[0]) * P::TF + (e % P::R[0]) * (P::N / P::R[0])) / (M / 64);
@@ -209,7 +217,7 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
 }
 
 template <class P>
-__global__ __launch_bounds__(P::TF, 2) void xcorr_half_kernel(
+__global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw,
@@ -267,6 +275,12 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
                        partials, nblocks, tw, wt);
     return hipGetLastError();
   }
+  if (M == 32768) {     // 16384-point halves, one block per CU
+    hipLaunchKernelGGL(xcorr_half_kernel<PlanX32k>, dim3((unsigned)nblocks), dim3(PlanX32k::TF), 0,
+                       st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
+                       partials, nblocks, tw, wt);
+    return hipGetLastError();
+  }
   auto run = [&](auto plan) {
     using PL = decltype(plan);
     auto k = xcorr_os_kernel<PL>;
@@ -283,7 +297,8 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
 // Wave geometry of the correlator's partials (see the header comment):
 // waves per block, rows Q and their stride; twiddle plan size.
 hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan) {
-  if (M == 16384) { *waves = Plan8192::TF / 64; *Q = 2 * Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
+  if (M == 32768) { *waves = PlanX32k::TF / 64; *Q = 2 * PlanX32k::E; *stride = PlanX32k::TF; *plan = -16384; }
+  else if (M == 16384) { *waves = Plan8192::TF / 64; *Q = 2 * Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 8192) { *waves = Plan8192::TF / 64; *Q = Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 4096) { *waves = Plan4096::TF / 64; *Q = Plan4096::E; *stride = Plan4096::TF; *plan = 4096; }
   else return hipErrorInvalidValue;

@@ -33,7 +33,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["ChainConfig", "HipBackend", "StreamChain", "combine_peaks", "HipPfbBackend",
-           "PfbChain"]
+           "PfbChain", "NativeChain", "Loopback"]
 
 
 @dataclass
@@ -366,6 +366,117 @@ class StreamChain:
         m, i, s1, s2 = combine_peaks(np.array(rows, dtype=object))
         nout = self.world * self.ny - self.L + 1
         return m, i, s1, s2, nout
+
+
+# ---------------------------------------------------------------------------
+# The same shard as one native object (C ABI vsig_chain_*, chain.hip)
+# ---------------------------------------------------------------------------
+class Loopback:
+    """In-process loopback transport (vsig_loopback_*): ranks as threads of one
+    process, halos copied device to device (tests run several ranks on one GPU)."""
+
+    def __init__(self, world: int):
+        import ctypes as C
+        from ._lib import load_library
+        self.lib = load_library()
+        h = C.c_void_p()
+        rc = self.lib.vsig_loopback_create(int(world), C.byref(h))
+        if rc:
+            raise ValueError(f"vsig_loopback_create: {rc}")
+        self.h, self.world = h, world
+
+    def transport(self, rank: int):
+        import ctypes as C
+        from ._lib import Transport
+        t = Transport()
+        rc = self.lib.vsig_loopback_transport(self.h, int(rank), C.byref(t))
+        if rc:
+            raise ValueError(f"vsig_loopback_transport: {rc}")
+        return t
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.lib.vsig_loopback_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class NativeChain:
+    """One rank of the time-chunk shard as a native vsig_chain: the same
+    stages, halos and global peak as StreamChain, driven by C++ (chain.hip)
+    through a vsig_transport (RCCL communicator, or Loopback for ranks in one
+    process).  Enqueues on the calling thread's context stream."""
+
+    def __init__(self, cfg: ChainConfig, device: int, rank: int = 0, world: int = 1, transport=None):
+        import ctypes as C
+        from ._lib import ChainConfig as CCfg, get_context
+        from .windows import get_window
+        cfg.validate(world)
+        self.ctx = get_context(device)
+        self.cfg, self.rank, self.world = cfg, rank, world
+        taps = np.ascontiguousarray(np.asarray(cfg.taps).ravel(), dtype=np.complex64)
+        w = get_window(cfg.window, cfg.nfft).astype(np.float32)
+        tm = (np.ascontiguousarray(np.asarray(cfg.template).ravel(), dtype=np.complex64)
+              if cfg.template is not None else None)
+        self._keep = (taps, w, tm, transport)
+        cc = CCfg(n_local=cfg.n_local, taps=taps.ctypes.data, ntaps=len(taps), decim=cfg.decim,
+                  nfft=cfg.nfft, window=w.ctypes.data,
+                  psd_scale=float(1.0 / float(np.sum(w, dtype=np.float64)) ** 2),
+                  tmpl=tm.ctypes.data if tm is not None else None,
+                  L=len(tm) if tm is not None else 0)
+        h = C.c_void_p()
+        self.ctx.check(self.ctx.lib.vsig_chain_create(self.ctx.h, C.byref(cc), rank, world,
+                                                      C.byref(transport) if transport is not None
+                                                      else None, C.byref(h)), "vsig_chain_create")
+        self.h = h
+        self.ny = cfg.n_local // cfg.decim
+        self.L = len(tm) if tm is not None else 0
+
+    def load(self, x: torch.Tensor):
+        """Copy this rank's input chunk (complex64, n_local samples) in."""
+        self.ctx.bind_stream()
+        if x.dtype != torch.complex64 or x.numel() != self.cfg.n_local or not x.is_contiguous():
+            raise ValueError("load: contiguous complex64 chunk of n_local samples")
+        dst = self.ctx.lib.vsig_chain_input(self.h)
+        self.ctx.check(self.ctx.lib.vsig_copy_dev(self.ctx.h, dst, x.data_ptr(), x.numel() * 8), "load")
+
+    def step(self):
+        self.ctx.bind_stream()
+        rc = self.ctx.lib.vsig_chain_step(self.h)
+        if rc:
+            raise RuntimeError(f"vsig_chain_step: {rc}: {self.ctx.lib.vsig_chain_last_error(self.h).decode()}")
+
+    def outputs(self):
+        """(filtered stream, frame-major spectra) copied into new device tensors."""
+        import ctypes as C
+        n, nf = C.c_int64(), C.c_int64()
+        yp = self.ctx.lib.vsig_chain_filtered(self.h, C.byref(n))
+        sp = self.ctx.lib.vsig_chain_spectra(self.h, C.byref(nf))
+        y = torch.empty(n.value, dtype=torch.complex64, device=f"cuda:{self.ctx.device}")
+        s = torch.empty(nf.value * self.cfg.nfft, dtype=torch.float32, device=y.device)
+        self.ctx.check(self.ctx.lib.vsig_copy_dev(self.ctx.h, y.data_ptr(), yp, y.numel() * 8), "y")
+        self.ctx.check(self.ctx.lib.vsig_copy_dev(self.ctx.h, s.data_ptr(), sp, s.numel() * 4), "sxx")
+        return y, s
+
+    def global_peak(self):
+        """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step."""
+        import ctypes as C
+        from ._lib import Peak
+        pk, nout = Peak(), C.c_int64()
+        rc = self.ctx.lib.vsig_chain_result(self.h, C.byref(pk), C.byref(nout))
+        if rc:
+            raise RuntimeError(f"vsig_chain_result: {rc}")
+        return pk.peak, int(pk.index), pk.sum_abs, pk.sum_abs2, int(nout.value)
+
+    def __del__(self):
+        try:
+            if self.h:
+                self.ctx.lib.vsig_chain_free(self.h)
+                self.h = None
+        except Exception:
+            pass
 
 
 # ---------------------------------------------------------------------------

@@ -29,7 +29,8 @@ import torch
 from . import _lib
 from .dsp import _device_c64, _is_dev, _ptr, peak_stats
 
-__all__ = ["apply_frequency_shift", "transplant_packet_in_vector", "mat2wv", "save_vector_wv",
+__all__ = ["apply_frequency_shift", "resample_signal", "transplant_packet_in_vector", "mat2wv",
+           "save_vector_wv",
            "load_packet", "load_packet_info", "save_vector", "read_mat", "write_mat_vector"]
 
 
@@ -62,6 +63,38 @@ def apply_frequency_shift(signal, freq_shift, sample_rate, start_index: int = 0)
 # ---------------------------------------------------------------------------
 # transplant_packet_in_vector — utils.py:1437-1501
 # ---------------------------------------------------------------------------
+def resample_signal(signal, orig_sr, target_sr):
+    """utils.py:107-118: ``scipy.signal.resample(signal, int(len * ratio))`` as
+    complex64 -- the spectrum of any length (Bluestein on the FFT engine,
+    bigfft.hip), its bins copied into the new length with scipy's Nyquist
+    rule, the inverse transform of any length.  Returns ``signal`` itself when
+    the rates are equal, like the reference."""
+    if orig_sr == target_sr:
+        return signal
+    dev = _is_dev(signal)
+    n = int(signal.shape[0]) if dev else len(signal)
+    num = int(n * (target_sr / orig_sr))
+    if num < 1:
+        raise ValueError(f"invalid number of data points ({num}) specified")
+    ctx = _lib.get_context()
+    if dev:
+        real = not signal.is_complex()
+        t = signal.to(torch.complex128 if signal.dtype in (torch.complex128, torch.float64)
+                      else torch.complex64).contiguous()
+    else:
+        a = np.asarray(signal)
+        real = not np.iscomplexobj(a)
+        wide = a.dtype in (np.complex128, np.float64, np.longdouble, np.clongdouble) or \
+            np.issubdtype(a.dtype, np.integer)
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.complex128 if wide else np.complex64)
+                             ).to(f"cuda:{ctx.device}")
+    code = "c128" if t.dtype == torch.complex128 else "c64"
+    y = torch.empty(num, dtype=torch.complex64, device=t.device)
+    ctx.check(ctx.lib.vsig_resample_dev(ctx.h, _lib.DTYPES[code], _ptr(t), n, num, 1 if real else 0,
+                                        _ptr(y)), "resample")
+    return y if dev else y.cpu().numpy()
+
+
 def _mean_power(t: torch.Tensor) -> np.float32:
     """np.mean(np.abs(seg) ** 2) of a complex64 segment: sum in double on the
     GPU, rounded to the float32 numpy returns."""
