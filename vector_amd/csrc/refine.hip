@@ -135,7 +135,7 @@ __device__ __forceinline__ long long item_output(const RefineGeom& g, long long 
 }
 
 // Stage 1: one block per (item, q) unit; lane l of every wave one output,
-// the 4 waves a quarter of the taps each (independent partial sums, loads
+// the 16 waves a sixteenth of the taps each (independent partial sums, loads
 // unrolled 8-deep so the loop is throughput- not latency-bound), combined in
 // LDS.  vals / idx / cv are indexed by u * 64 + l, u = item slot * Q + q.
 template <class T>
@@ -165,8 +165,10 @@ __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __r
   im = i0 + i1;
 }
 
+constexpr int kS1Waves = 16;
+
 template <class T>
-__global__ __launch_bounds__(256) void refine_stage1(const T* __restrict__ a, const T* __restrict__ v,
+__global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restrict__ a, const T* __restrict__ v,
                                                      RefineGeom g, const long long* __restrict__ items,
                                                      long long cap, RefineKeys* __restrict__ keys,
                                                      double* __restrict__ vals,
@@ -176,7 +178,7 @@ __global__ __launch_bounds__(256) void refine_stage1(const T* __restrict__ a, co
   if (keys->status || cnt == 0) return;
   const long long nunits = (cnt < cap ? cnt : cap) * g.Q;
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __shared__ double pr[4][64], pi[4][64];
+  __shared__ double pr[kS1Waves][64], pi[kS1Waves][64];
   for (long long u = blockIdx.x; u < nunits; u += gridDim.x) {   // uniform per block
     const long long item = items[u / g.Q];
     const int q = (int)(u % g.Q);
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(256) void refine_stage1(const T* __restrict__ a, co
       const long long i = g.F + o;
       long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
-      const long long span = (k1 - k0 + 3) / 4;          // this wave's quarter of the taps
+      const long long span = (k1 - k0 + kS1Waves - 1) / kS1Waves;   // this wave's share
       const long long q0 = k0 + w * span;
       const long long q1 = q0 + span < k1 ? q0 + span : k1;
       if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im);
@@ -195,8 +197,10 @@ __global__ __launch_bounds__(256) void refine_stage1(const T* __restrict__ a, co
     pi[w][l] = im;
     __syncthreads();
     if (w == 0) {
-      re = (pr[0][l] + pr[1][l]) + (pr[2][l] + pr[3][l]);
-      im = (pi[0][l] + pi[1][l]) + (pi[2][l] + pi[3][l]);
+      re = 0.0;
+      im = 0.0;
+#pragma unroll
+      for (int q2 = 0; q2 < kS1Waves; ++q2) { re += pr[q2][l]; im += pi[q2][l]; }
       const double m2 = o >= 0 ? re * re + im * im : -1.0;
       const long long e = u * 64 + l;
       vals[e] = m2;
@@ -354,14 +358,14 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   if (r.c128) {
     const double2* a = static_cast<const double2*>(r.a);
     const double2* v = static_cast<const double2*>(r.v);
-    hipLaunchKernelGGL(refine_stage1<double2>, dim3(g1), dim3(256), 0, st, a, v, g, items,
+    hipLaunchKernelGGL(refine_stage1<double2>, dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
                        r.cap_items, keys, vals, oidx, cv);
     hipLaunchKernelGGL(refine_stage2<double2>, dim3(g2), dim3(256), 0, st, a, v, g, r.cap_items,
                        r.eps2, keys, vals, oidx, cv);
   } else {
     const float2* a = static_cast<const float2*>(r.a);
     const float2* v = static_cast<const float2*>(r.v);
-    hipLaunchKernelGGL(refine_stage1<float2>, dim3(g1), dim3(256), 0, st, a, v, g, items,
+    hipLaunchKernelGGL(refine_stage1<float2>, dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
                        r.cap_items, keys, vals, oidx, cv);
     hipLaunchKernelGGL(refine_stage2<float2>, dim3(g2), dim3(256), 0, st, a, v, g, r.cap_items,
                        r.eps2, keys, vals, oidx, cv);
