@@ -228,6 +228,22 @@ struct WaveSync : P {
   static_assert(P::TF <= 64, "wave-private frames only");
   static constexpr bool WAVE_SYNC = true;
 };
+// The first passes of an N-point plan only (product of the radices L divides
+// N): the engine stops with the L-point transforms of the N / L polyphase
+// components x[k + (N/L) m] in registers, thread t holding butterfly j's
+// outputs b[(j/Ns)*Ns*R + (j mod Ns) + r*Ns] of the last pass -- i.e.
+// component k = j / Ns, bins (j mod Ns) + r*Ns (Stockham after L points).
+// The decimating FIR replaces the N-point transform's remaining passes, the
+// filter multiply and the fold by one multiply-sum over the components.
+template <class P>
+struct Partial : P {
+  static constexpr bool valid() {
+    int prod = 1;
+    for (int q = 0; q < P::NP; ++q) { if (P::E % P::R[q]) return false; prod *= P::R[q]; }
+    return P::N % prod == 0;
+  }
+};
+
 template <class P, class = void>
 struct wave_sync_of { static constexpr bool value = false; };
 template <class P>
@@ -656,6 +672,10 @@ using Plan2048s = Plan<2048, 32, 8, 32, 8>;
 // D = 2 / 4, same 64 threads): thread t holds bins t + 64 r of both.
 using Plan512d = Plan<512, 8, 8, 8, 8>;
 using Plan256d = Plan<256, 4, 4, 4, 4, 4>;
+// Polyphase front of the D = 4 decimating FIR: the two radix-16 passes of a
+// 1024-point transform = the 256-point spectra of its 4 polyphase components
+// (pass-1 twiddles = Plan256's table).
+using Plan1024q = Partial<Plan<1024, 16, 16, 16>>;
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

@@ -149,6 +149,133 @@ __global__ __launch_bounds__(P::TF) void fir_dec_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// D = 4, polyphase form.  The 1024-point segment transform of fir_dec_kernel
+// followed by x H and the fold by 4 equals, per decimated bin j < 256,
+//   Yd[j] = sum_k U_k[j] G_k[j],   U_k = FFT_256(x[k + 4 m]),
+//   G_k[j] = W_1024^{k j} sum_s W_4^{k s} Hs[j + 256 s]        (fir_poly_gtable)
+// so the segment needs only the two radix-16 passes of Plan1024q (thread t
+// ends with U_{t/16}[(t%16) + 16 r], r < 16): one LDS exchange and one
+// twiddled pass fewer.  The sum over k = t/16 runs across the lanes t, t^16,
+// t^32, t^48 as a reduce-scatter with v_permlane32_swap / v_permlane16_swap
+// (no LDS): afterwards lane t holds Yd[tq + 64 i], i < 4, with tq = t with
+// bits 4 and 5 exchanged -- Plan256d's operand layout for thread tq, which
+// runs the inverse transform and the stores under that index.
+// ---------------------------------------------------------------------------
+// a + b across lane pairs (l, l ^ 32): lanes < 32 return a(l) + a(l + 32),
+// lanes >= 32 return b(l - 32) + b(l).
+__device__ __forceinline__ float2 swap32_add(float2 a, float2 b) {
+  const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  return cadd(make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0])),
+              make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
+}
+// the same across (l, l ^ 16): lanes with bit 4 clear return a(l) + a(l + 16),
+// the others b(l - 16) + b(l).
+__device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
+  const auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
+  const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
+  return cadd(make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0])),
+              make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
+}
+
+template <bool MIX = false>
+__global__ __launch_bounds__(64) void fir_poly_kernel(
+    const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
+    long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
+    const float2* __restrict__ twd, MixArgs mix) {
+  using P = Plan1024q;
+  using PD = Plan256d;
+  constexpr int D = 4;
+  static_assert(P::TF == 64 && P::E == 16 && P::NP == 2 && P::R[1] == 16 && PD::E == 4,
+                "lane layout of the reduce-scatter");
+  __shared__ float2 lds[P::LDS];
+  const int t = threadIdx.x;
+  const long long b = xcd_remap(blockIdx.x, gridDim.x);
+  if (2 * b >= nblocks) return;
+  const long long nloc = n - g0;
+  const int tq = (t & 15) | ((t & 16) << 1) | ((t & 32) >> 1);
+  float2 wa[nanch_total<P>()];
+  load_anchors<P>(wa, tw, t);
+  float2 wr[rtw_total<PD>()];
+  load_rtw<PD>(wr, twd, tq);
+  float2 a[P::E], d[P::E];
+  if constexpr (MIX) {
+    load_segment_mix<P>(a, x, g0 + (2 * b) * hop - lo2, n, t, mix);
+    load_segment_mix<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t, mix);
+  } else {
+    load_segment<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
+    load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
+  }
+  launder_anchors<P>(wa);
+  fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+  const float2* Gk = G + (t >> 4) * 256 + (t & 15);
+  float2 ua[PD::E], ud[PD::E];
+#pragma unroll
+  for (int i = 0; i < PD::E; ++i) {
+    float2 pa[4], pd[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const float2 g = Gk[16 * (4 * i + q)];
+      pa[q] = cmul(a[4 * i + q], g);
+      pd[q] = cmul(d[4 * i + q], g);
+    }
+    const float2 sa0 = swap32_add(pa[0], pa[1]), sa1 = swap32_add(pa[2], pa[3]);
+    const float2 sd0 = swap32_add(pd[0], pd[1]), sd1 = swap32_add(pd[2], pd[3]);
+    ua[i] = cconj(swap16_add(sa0, sa1));
+    ud[i] = cconj(swap16_add(sd0, sd1));
+  }
+  fft_pair<PD>(ua, ud, lds, TwRegs{wr}, tq);
+  const int n0 = lo2 / D, n1 = (lo2 + (int)hop) / D;
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const long long bb = 2 * b + f;
+    const long long gb = bb * hop - lo2;          // chunk output of circular index 0
+    float2* yb = y + bb * (hop / D) - n0;
+    const float2* u = f ? ud : ua;
+#pragma unroll
+    for (int e = 0; e < PD::E; ++e) {
+      const int i = out_index<PD>(tq, e);
+      if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, cconj(u[e]));
+    }
+  }
+}
+
+// G_k[j] (see fir_poly_kernel) from Hs = FFT_1024(h) / 1024, in double.
+__global__ void fir_poly_gtable(const float2* __restrict__ Hs, float2* __restrict__ G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 1024) return;
+  const int k = i >> 8, j = i & 255;
+  double re = 0.0, im = 0.0;
+  for (int s = 0; s < 4; ++s) {
+    double sn, cs;
+    sincospi(-2.0 * (double)(k * (j + 256 * s)) / 1024.0, &sn, &cs);
+    const float2 h = Hs[j + 256 * s];
+    re += (double)h.x * cs - (double)h.y * sn;
+    im += (double)h.x * sn + (double)h.y * cs;
+  }
+  G[i] = make_float2((float)re, (float)im);
+}
+
+hipError_t launch_fir_poly_gtable(const float2* Hs, float2* G, hipStream_t st) {
+  hipLaunchKernelGGL(fir_poly_gtable, dim3(4), dim3(256), 0, st, Hs, G);
+  return hipGetLastError();
+}
+
+hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const float2* G, int lo2,
+                           long long hop, float2* y, const float2* tw, const float2* twd,
+                           hipStream_t st, const MixArgs* mix) {
+  if (n - g0 <= 0) return hipSuccess;
+  const long long nblocks = (n - g0 + hop - 1) / hop;
+  const dim3 g((unsigned)((nblocks + 1) / 2)), blk(64);
+  const MixArgs m = mix ? *mix : MixArgs{};
+  if (mix)
+    hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+  else
+    hipLaunchKernelGGL(fir_poly_kernel<false>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+  return hipGetLastError();
+}
+
 hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
                           int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
                           hipStream_t st, const MixArgs* mix) {

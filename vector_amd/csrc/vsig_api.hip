@@ -51,6 +51,7 @@ struct vsig_fir {
   int ntaps, decim, M;
   long long hop;
   float2* Hs;
+  float2* G = nullptr;   // D = 4 polyphase component filters (M = 1024)
 };
 
 // A correlation template: L <= 8192 one spectrum of M points; longer
@@ -682,10 +683,20 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
   if (e != hipSuccess) { (void)hipFree(hd); return fail(c, VSIG_E_HIP, hipGetErrorString(e)); }
   float2* Hs = nullptr;
   int rc = make_spectrum(c, hd, ntaps, M, &Hs);
+  float2* G = nullptr;
+  if (!rc && M == 1024 && decim == 4) {
+    hipError_t ge = hipMalloc(&G, 1024 * sizeof(float2));
+    if (ge == hipSuccess) ge = vsig::launch_fir_poly_gtable(Hs, G, c->stream);
+    if (ge != hipSuccess) rc = fail(c, VSIG_E_HIP, hipGetErrorString(ge));
+  }
   (void)hipStreamSynchronize(c->stream);
   (void)hipFree(hd);
-  if (rc) return rc;
-  *out = new vsig_fir{c, ntaps, decim, M, hop, Hs};
+  if (rc) {
+    (void)hipFree(Hs);
+    (void)hipFree(G);
+    return rc;
+  }
+  *out = new vsig_fir{c, ntaps, decim, M, hop, Hs, G};
   return VSIG_OK;
 }
 
@@ -693,6 +704,7 @@ void vsig_fir_free(vsig_fir* f) {
   if (!f) return;
   (void)hipStreamSynchronize(f->ctx->stream);
   (void)hipFree(f->Hs);
+  (void)hipFree(f->G);
   delete f;
 }
 
@@ -708,11 +720,20 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
   if (f->M == 1024 && (f->decim == 2 || f->decim == 4)) {
     // decimation in the frequency domain: M/D-point inverse transforms
     const float2* twd;
-    if ((rc = get_twiddles(c, -1024, &tw)) || (rc = get_twiddles(c, -1024 / f->decim, &twd))) return rc;
     const int D = f->decim;
     const int lo2 = (f->ntaps - 1 + D - 1) / D * D;
     const long long hop = (long long)(f->M - lo2) / D * D;
     if (hop < D) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
+#ifndef VSIG_FIR_DEC_FOLD
+    if (f->G) {      // D = 4: polyphase form (fir_poly_kernel)
+      if ((rc = get_twiddles(c, 256, &tw)) || (rc = get_twiddles(c, -256, &twd))) return rc;
+      Timed t(c, "fir");
+      HIPCHK(c, vsig::launch_fir_poly((const float2*)x, nhist + n, nhist, f->G, lo2, hop, (float2*)y, tw,
+                                      twd, c->stream, mix));
+      return VSIG_OK;
+    }
+#endif
+    if ((rc = get_twiddles(c, -1024, &tw)) || (rc = get_twiddles(c, -1024 / f->decim, &twd))) return rc;
     Timed t(c, "fir");
     HIPCHK(c, vsig::launch_fir_dec(D, (const float2*)x, nhist + n, nhist, f->Hs, lo2, hop, (float2*)y,
                                    tw, twd, c->stream, mix));

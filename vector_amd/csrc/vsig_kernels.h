@@ -105,6 +105,13 @@ hipError_t launch_spectrum_prep(int N, const float2* u, int len, float gain, flo
 hipError_t launch_fir_dec(int decim, const float2* x, long long n, long long g0, const float2* Hs,
                           int lo2, long long hop, float2* y, const float2* tw, const float2* twd,
                           hipStream_t st, const MixArgs* mix = nullptr);
+// D = 4 at M = 1024 in polyphase form (fir.hip fir_poly_kernel): G = the
+// 4 x 256 component filters from Hs (launch_fir_poly_gtable), tw = Plan256's
+// table, twd = Plan256d's.
+hipError_t launch_fir_poly_gtable(const float2* Hs, float2* G, hipStream_t st);
+hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const float2* G, int lo2,
+                           long long hop, float2* y, const float2* tw, const float2* twd,
+                           hipStream_t st, const MixArgs* mix = nullptr);
 // Overlap-save FIR, M in {1024, 4096, 8192, 16384} (mix: M = 1024 only).
 hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, const float2* Hs,
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
