@@ -219,6 +219,51 @@ struct Plan {
 
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
+// Per-plan LDS exchange geometry.  Default: 1 float2 of padding per 16, every
+// pass's butterfly j = t + b TF.  A plan may pad 1 per 2^PADSH instead and set
+// SIGMA: the first and the last pass then run butterfly j = sigma(t) + b TF,
+//   sigma(t) = (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1)
+// (lanes 0-15 take the even j of their 32-lane half, lanes 16-31 the odd).
+// Why (Plan8192x): the first pass's stride-16 scatter stores (16 j + r,
+// ds_write_b64: 16-lane groups, banks mod 32 dwords) need the padding to
+// differ across the group's j, and the later passes' reads (t + 256 m,
+// ds_read_b64: 32-lane groups, banks mod 64 dwords) need it equal across a
+// 32-lane run.  1 per 16 serves the stores but puts lanes 0 and 31 of every
+// read group on one bank (one extra cycle per ds_read_b64); 1 per 32 serves
+// the reads, and sigma gives each store group 16 j of one parity, whose
+// padding j / 2 is again distinct.  The operand / result layouts
+// (in_index / out_index) follow sigma.
+template <class P, class = void>
+struct padsh_of { static constexpr int value = 4; };
+template <class P>
+struct padsh_of<P, decltype(void(P::PADSH))> { static constexpr int value = P::PADSH; };
+template <class P, class = void>
+struct sigma_of { static constexpr bool value = false; };
+template <class P>
+struct sigma_of<P, decltype(void(P::SIGMA))> { static constexpr bool value = P::SIGMA; };
+
+template <class P>
+__device__ __forceinline__ int lpadp(int i) { return i + (i >> padsh_of<P>::value); }
+template <class P>
+__device__ __forceinline__ int tmap(int t) {
+  if constexpr (sigma_of<P>::value) return (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1);
+  else return t;
+}
+// thread t's butterfly index base in pass p
+template <class P, int p>
+__device__ __forceinline__ int tpass(int t) {
+  if constexpr (p == 0 || p == P::NP - 1) return tmap<P>(t);
+  else return t;
+}
+
+template <class P>
+struct Swz : P {
+  static_assert(P::TF % 64 == 0 && (P::N / P::R[0]) % 32 == 0, "sigma permutes 32-lane runs");
+  static constexpr int PADSH = 5;
+  static constexpr bool SIGMA = true;
+  static constexpr int LDS = P::N + P::N / 32;
+};
+
 // A plan whose frame is owned by one wave and whose LDS slice is private to
 // that wave: the engine's exchanges then need only a wave barrier (LDS
 // requests of one wave complete in issue order), so the waves of a
@@ -327,7 +372,7 @@ __device__ __forceinline__ void load_rtw(float2* w, const float2* __restrict__ t
     constexpr int R = P::R[p], Ns = P::ns(p), NB = rtw_nb<P>(p);
     static_for<0, NB>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
-      const int k = (t + b * P::TF) & (Ns - 1);
+      const int k = (tpass<P, p>(t) + b * P::TF) & (Ns - 1);
 #pragma unroll
       for (int r = 1; r < R; ++r) w[rtw_off<P>(p) + b * (R - 1) + r - 1] = tw[P::twoff(p) + (r - 1) * Ns + k];
     });
@@ -353,7 +398,7 @@ __device__ __forceinline__ void load_anchors(float2* wa, const float2* __restric
     constexpr int R = P::R[p], Ns = P::ns(p), B = P::E / R, NA = nanch<P>(p);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
-      const int k = (t + b * P::TF) & (Ns - 1);
+      const int k = (tpass<P, p>(t) + b * P::TF) & (Ns - 1);
       static_for<0, NA>([&](auto ai) {
         constexpr int a = decltype(ai)::value;
         constexpr int r = a == 0 ? 1 : 8 * a;
@@ -374,7 +419,7 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
   if constexpr (std::is_same<TW, TwTable>::value) {
-    const unsigned j = (unsigned)t + b * P::TF;
+    const unsigned j = (unsigned)tpass<P, p>(t) + b * P::TF;
     const unsigned k = j & (Ns - 1);
     const float2* twp = tws.tw + P::twoff(p);
 #pragma unroll
@@ -387,7 +432,7 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
   } else if constexpr (std::is_same<TW, TwLds>::value) {
     constexpr int S = tw2_shift<P>();
     constexpr int stride = P::N / (Ns * R);       // W_{Ns R}^{rk} = W_N^{rk stride}
-    const int j = t + b * P::TF;
+    const int j = tpass<P, p>(t) + b * P::TF;
     const int k = j & (Ns - 1);
     const float2* A = tws.t2;
     const float2* Bt = tws.t2 + tw2_hi<P>();
@@ -436,10 +481,29 @@ __device__ __forceinline__ void fft_stage(float2* v, TW tws, int t, H hook = H{}
 // lpad(base + c) for a compile-time c: multiples of 16 become an immediate
 // offset from lpad(base) (lpad(b + 16m) = lpad(b) + 17m), so a pass needs one
 // LDS base address per butterfly instead of one per element.
-template <int C>
+template <class P, int C>
 __device__ __forceinline__ int lpad_off(int base, int base_pad) {
-  if constexpr (C % 16 == 0) return base_pad + C + C / 16;
-  else return lpad(base + C);
+  constexpr int S = padsh_of<P>::value;
+  if constexpr (C % (1 << S) == 0) return base_pad + C + (C >> S);
+  else return lpadp<P>(base + C);
+}
+
+// Padded LDS index of butterfly j's output 0 in pass p, such that output r
+// sits at store_base + C + (C >> S), C = r Ns (S = padsh): the destination
+// base + C, base = hi + lo with hi = (j / Ns) Ns R, lo = j mod Ns, pads as
+//   Ns >= 2^S : lpad(base) + C + (C >> S)             (C a multiple of 2^S);
+//   Ns <  2^S : base + (hi >> S) + C + (C >> S)       (lo + C never carries
+//               past bit S into hi's multiple of 2^S, or stays below Ns R <=
+//               2^S) -- one address per butterfly, immediate offsets per r.
+template <class P, int p>
+__device__ __forceinline__ int store_base(int j) {
+  constexpr int R = P::R[p];
+  constexpr int Ns = P::ns(p);
+  constexpr int S = padsh_of<P>::value;
+  const int hi = (j / Ns) * Ns * R;
+  const int base = hi + (j & (Ns - 1));
+  if constexpr (Ns >= (1 << S)) return lpadp<P>(base);
+  else return base + (hi >> S);
 }
 
 template <class P, int p>
@@ -449,12 +513,12 @@ __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
   constexpr int B = P::E / R;
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
-    const int j = t + b * P::TF;
-    const int base = (j / Ns) * Ns * R + (j & (Ns - 1));
-    const int bp = lpad(base);
+    const int j = tpass<P, p>(t) + b * P::TF;
+    const int bp = store_base<P, p>(j);
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      lds[lpad_off<r * Ns>(base, bp)] = v[b * R + r];
+      constexpr int C = r * Ns;
+      lds[bp + C + (C >> padsh_of<P>::value)] = v[b * R + r];
     });
   });
 }
@@ -463,12 +527,13 @@ template <class P, int p>
 __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
-  const int tp = lpad(t);
+  const int tl = tpass<P, p>(t);
+  const int tp = lpadp<P>(tl);
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      v[b * R + r] = lds[lpad_off<b * P::TF + r * (P::N / R)>(t, tp)];
+      v[b * R + r] = lds[lpad_off<P, b * P::TF + r * (P::N / R)>(tl, tp)];
     });
   });
 }
@@ -483,12 +548,12 @@ __device__ __forceinline__ void fft_store_c(const float2* v, float* lds, int t) 
   constexpr int B = P::E / R;
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
-    const int j = t + b * P::TF;
-    const int base = (j / Ns) * Ns * R + (j & (Ns - 1));
-    const int bp = lpad(base);
+    const int j = tpass<P, p>(t) + b * P::TF;
+    const int bp = store_base<P, p>(j);
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      lds[lpad_off<r * Ns>(base, bp)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
+      constexpr int O = r * Ns;
+      lds[bp + O + (O >> padsh_of<P>::value)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
     });
   });
 }
@@ -497,12 +562,13 @@ template <class P, int p, int C>
 __device__ __forceinline__ void fft_load_c(float2* v, const float* lds, int t) {
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
-  const int tp = lpad(t);
+  const int tl = tpass<P, p>(t);
+  const int tp = lpadp<P>(tl);
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      const float f = lds[lpad_off<b * P::TF + r * (P::N / R)>(t, tp)];
+      const float f = lds[lpad_off<P, b * P::TF + r * (P::N / R)>(tl, tp)];
       if constexpr (C == 0) v[b * R + r].x = f; else v[b * R + r].y = f;
     });
   });
@@ -642,12 +708,12 @@ __device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW t
 template <class P>
 __device__ __forceinline__ int in_index(int t, int e) {          // pass-0 operand e of thread t
   constexpr int R = P::R[0];
-  return t + (e / R) * P::TF + (e % R) * (P::N / R);
+  return tmap<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
 }
 template <class P>
 __device__ __forceinline__ int out_index(int t, int e) {         // result e of thread t
   constexpr int R = P::RL;
-  return t + (e / R) * P::TF + (e % R) * (P::N / R);
+  return tmap<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
 }
 
 // ---------------------------------------------------------------------------
@@ -676,6 +742,8 @@ using Plan256d = Plan<256, 4, 4, 4, 4, 4>;
 // 1024-point transform = the 256-point spectra of its 4 polyphase components
 // (pass-1 twiddles = Plan256's table).
 using Plan1024q = Partial<Plan<1024, 16, 16, 16>>;
+// The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
+using Plan8192x = Swz<Plan8192>;
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

@@ -24,7 +24,9 @@ __device__ __forceinline__ void psd_load(float2* v, const float2* __restrict__ x
 
 // Plans of >= 256 threads per frame (nfft >= 4096): two frames per block
 // through fft_pair (the LDS stores of one frame overlap the other's
-// butterflies), twiddles from register anchors.
+// butterflies), twiddles from register anchors.  (The conflict-free Plan8192x
+// exchange that the correlator uses measured slower here -- 1.43 vs 1.17 ms at
+// config 5: at 254 VGPRs the sigma map's extra registers spill.)
 template <class P>
 __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
     const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,

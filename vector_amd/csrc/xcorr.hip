@@ -124,6 +124,11 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
 // per 2^28 samples against 1.42 ms for the M = 16384 kernel (r02_v6 A/B), so
 // shorter templates keep M = 16384.
 using PlanX32k = Plan16384w;
+#ifndef VSIG_NO_SWZ
+using PlanX16k = Plan8192x;     // conflict-free exchanges (fft_engine.hpp Swz)
+#else
+using PlanX16k = Plan8192;
+#endif
 
 template <class P, int M>
 constexpr int half_root(int e) {
@@ -238,7 +243,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   };
   float2 a[P::E], d[P::E];
   load_halves<P>(a, d, s, b * hop - off, n, t);
-  const float2 w = wt[t];
+  const float2 w = wt[tmap<P>(t)];      // W_M^j, j = in_index(t, 0)
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 x0 = a[e], x1 = d[e];
@@ -270,7 +275,7 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
   if (M == 16384) {
-    hipLaunchKernelGGL(xcorr_half_kernel<Plan8192>, dim3((unsigned)nblocks), dim3(Plan8192::TF), 0,
+    hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
                        partials, nblocks, tw, wt);
     return hipGetLastError();
