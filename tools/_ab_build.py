@@ -9,6 +9,7 @@ VARIANTS = {
     "libvsig_x32": ("VSIG_XCORR_BIG_FROM=2049",),
     "libvsig_noswz": ("VSIG_NO_SWZ",),
     "libvsig_fold": ("VSIG_FIR_DEC_FOLD",),
+    "libvsig_firko": ("VSIG_FIR_KO",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

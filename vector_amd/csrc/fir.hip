@@ -179,6 +179,11 @@ __device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
               make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
 }
 
+// Tuning builds: VSIG_FIR_KO skips both transform pairs (memory-only
+// knock-out, outputs wrong): 3.85-3.94 ms at config 5 against 4.32-4.37 ms
+// for the kernel (profiles/r02_v12_ab.txt), i.e. the loads / stores of this
+// access pattern alone run at 5.5 TB/s and the transforms add ~0.45 ms.
+
 template <bool MIX = false>
 __global__ __launch_bounds__(64) void fir_poly_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
@@ -208,7 +213,9 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
     load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
   }
   launder_anchors<P>(wa);
+#ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+#endif
   const float2* Gk = G + (t >> 4) * 256 + (t & 15);
   float2 ua[PD::E], ud[PD::E];
 #pragma unroll
@@ -225,7 +232,9 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
     ua[i] = cconj(swap16_add(sa0, sa1));
     ud[i] = cconj(swap16_add(sd0, sd1));
   }
+#ifndef VSIG_FIR_KO
   fft_pair<PD>(ua, ud, lds, TwRegs{wr}, tq);
+#endif
   const int n0 = lo2 / D, n1 = (lo2 + (int)hop) / D;
 #pragma unroll
   for (int f = 0; f < 2; ++f) {

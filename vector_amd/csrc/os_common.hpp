@@ -28,19 +28,19 @@ __device__ __forceinline__ void st_stream(float2* p, float2 v) {
 // Pass-0 operands of an overlap-save segment x[s0 .. s0 + N) with zero fill
 // outside [0, n).  The block-uniform base keeps the address in SGPRs; interior
 // segments (the common case) skip the per-element bounds test.
-template <class P>
+template <class P, bool NT = false>
 __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict__ x,
                                              long long s0, long long n, int t) {
   const float2* base = x + s0;
   if (s0 >= 0 && s0 + P::N <= n) {
 #pragma unroll
-    for (int e = 0; e < P::E; ++e) v[e] = ld_stream(base + (unsigned)in_index<P>(t, e));
+    for (int e = 0; e < P::E; ++e) v[e] = ld_stream<NT>(base + (unsigned)in_index<P>(t, e));
   } else {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = in_index<P>(t, e);
       const long long xi = s0 + i;
-      v[e] = (xi >= 0 && xi < n) ? ld_stream(base + i) : make_float2(0.f, 0.f);
+      v[e] = (xi >= 0 && xi < n) ? ld_stream<NT>(base + i) : make_float2(0.f, 0.f);
     }
   }
 }
