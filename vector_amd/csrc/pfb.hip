@@ -122,7 +122,10 @@ static void launch_pfb_t(const float2* x, long long n, const float* h, long long
   constexpr int step = E * (PT / cgcd(E, PT));
   // frames per group: a multiple of the unrolled step, so the (PT-1)-row ring
   // prologue stays a small fraction of the group's reads
-  constexpr long long want = 64;
+#ifndef VSIG_PFB_FPG
+#define VSIG_PFB_FPG 64
+#endif
+  constexpr long long want = VSIG_PFB_FPG;
   const long long fpg = ((want + step - 1) / step) * step;
   const long long groups = (M + fpg - 1) / fpg;
   const long long blocks = (groups + G - 1) / G;
