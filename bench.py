@@ -130,8 +130,13 @@ def load_traffic(key):
     """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary
     (profiles/pmc_*.json, corrected as MI355X_MICROARCH.md §HBM prescribes)."""
     import glob
+    import re
+
+    def order(p):       # newest profile round / version last (r02_v14 after r02_v8)
+        m = re.search(r"_r(\d+)_v(\d+)", os.path.basename(p))
+        return (int(m.group(1)), int(m.group(2))) if m else (0, 0)
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json")), key=order):
         try:
             d = json.load(open(p))
         except Exception:
@@ -528,6 +533,7 @@ def run_pfb(args, world, rank, local, dev):
                 "traffic_source": pmc["source"] if pmc else None}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
+        from oracle import ref        # the CPU baseline leg only
         ns = 1 << 22
         xs = ref.synth_iq(ns, seed=99)
         t0 = time.perf_counter()

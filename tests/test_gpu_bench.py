@@ -1,0 +1,34 @@
+"""bench.py end to end on the GPU at small sizes, every workload with its CPU
+baseline leg: the JSON contract the driver reads (metric / value / roofline /
+cpu_baseline / check) and the planted-preamble check."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("workload", ["c5", "c2", "sync", "pfb"])
+def test_bench_workload_small(gpu, workload):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload,
+           "--samples", str(1 << 22), "--steps", "2", "--warmup", "1",
+           "--cpu-samples", str(1 << 16), "--cpu-workers", "2"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
+    d = json.loads(line)
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+              "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+              "roofline", "cpu_baseline", "check"):
+        assert k in d, k
+    assert d["n_gpus"] == 1 and d["steps"] == 2 and d["value"] > 0
+    assert d["check"]["ok"], d["check"]
+    roof = d["roofline"]
+    assert roof["bound"] == "hbm" and 0 < roof["frac"] < 1 and roof["avg_launch_ms"] > 0
+    cpu = d["cpu_baseline"]
+    assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
