@@ -10,6 +10,7 @@ VARIANTS = {
     "libvsig_noswz": ("VSIG_NO_SWZ",),
     "libvsig_fold": ("VSIG_FIR_DEC_FOLD",),
     "libvsig_firko": ("VSIG_FIR_KO",),
+    "libvsig_nox4": ("VSIG_NO_X4",),
     "libvsig_pfb128": ("VSIG_PFB_FPG=128",),
     "libvsig_pfb256": ("VSIG_PFB_FPG=256",),
     "libvsig_pfb512": ("VSIG_PFB_FPG=512",),

@@ -220,49 +220,74 @@ struct Plan {
 __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 
 // Per-plan LDS exchange geometry.  Default: 1 float2 of padding per 16, every
-// pass's butterfly j = t + b TF.  A plan may pad 1 per 2^PADSH instead and set
-// SIGMA: the first and the last pass then run butterfly j = sigma(t) + b TF,
-//   sigma(t) = (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1)
-// (lanes 0-15 take the even j of their 32-lane half, lanes 16-31 the odd).
-// Why (Plan8192x): the first pass's stride-16 scatter stores (16 j + r,
-// ds_write_b64: 16-lane groups, banks mod 32 dwords) need the padding to
-// differ across the group's j, and the later passes' reads (t + 256 m,
-// ds_read_b64: 32-lane groups, banks mod 64 dwords) need it equal across a
-// 32-lane run.  1 per 16 serves the stores but puts lanes 0 and 31 of every
-// read group on one bank (one extra cycle per ds_read_b64); 1 per 32 serves
-// the reads, and sigma gives each store group 16 j of one parity, whose
-// padding j / 2 is again distinct.  The operand / result layouts
-// (in_index / out_index) follow sigma.
+// pass's butterfly j = t + b TF.  A plan may pad 1 per 2^PADSH instead and
+// give its first pass (MAP0) and its last pass (MAPL) a lane map m(t): the
+// pass then runs butterfly j = m(t) + b TF (the passes in between keep
+// j = t; a pass's thread map changes only who computes which butterfly, the
+// LDS image between passes is the same).  Maps:
+//   kMapId    m(t) = t;
+//   kMapSigma m(t) = (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1)
+//             (lanes 0-15 take the even j of their 32-lane half, lanes 16-31
+//             the odd);
+//   kMapPair  m(t) = ((t & 31) << 1) | (t >> 5)   (TF = 64: lane l < 32 takes
+//             j = 2l, lane l + 32 takes j = 2l + 1) -- the layout a 16-byte
+//             load (samples 2l, 2l + 1) reaches after one v_permlane32_swap
+//             (load_segment_x4).
+// Why padding 1 per 32 with sigma or pair maps (Plan8192x, the FIR plans): the
+// first pass's stride-R scatter stores (R j + r, ds_write_b64: 16-lane groups,
+// banks mod 32 dwords) need the padding to differ across the group's j, and
+// the later passes' reads (t + (N/R) m, ds_read_b64: 32-lane groups, banks mod
+// 64 dwords) need it equal across a 32-lane run.  1 per 16 serves the stores
+// but puts lanes 0 and 31 of every read group on one bank (one extra cycle
+// per ds_read_b64); 1 per 32 serves the reads, and both maps give each store
+// group 16 j of one parity, whose padding j / 2 is again distinct.  The
+// operand / result layouts follow the maps (in_index: MAP0, out_index: MAPL).
+constexpr int kMapId = 0, kMapSigma = 1, kMapPair = 2;
 template <class P, class = void>
 struct padsh_of { static constexpr int value = 4; };
 template <class P>
 struct padsh_of<P, decltype(void(P::PADSH))> { static constexpr int value = P::PADSH; };
 template <class P, class = void>
-struct sigma_of { static constexpr bool value = false; };
+struct map0_of { static constexpr int value = kMapId; };
 template <class P>
-struct sigma_of<P, decltype(void(P::SIGMA))> { static constexpr bool value = P::SIGMA; };
+struct map0_of<P, decltype(void(P::MAP0))> { static constexpr int value = P::MAP0; };
+template <class P, class = void>
+struct mapl_of { static constexpr int value = kMapId; };
+template <class P>
+struct mapl_of<P, decltype(void(P::MAPL))> { static constexpr int value = P::MAPL; };
 
 template <class P>
 __device__ __forceinline__ int lpadp(int i) { return i + (i >> padsh_of<P>::value); }
-template <class P>
-__device__ __forceinline__ int tmap(int t) {
-  if constexpr (sigma_of<P>::value) return (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1);
+template <int MAP>
+__device__ __forceinline__ int lane_map(int t) {
+  if constexpr (MAP == kMapSigma) return (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1);
+  else if constexpr (MAP == kMapPair) return ((t & 31) << 1) | (t >> 5);
   else return t;
 }
+template <class P>
+__device__ __forceinline__ int tmap0(int t) { return lane_map<map0_of<P>::value>(t); }
+template <class P>
+__device__ __forceinline__ int tmapl(int t) { return lane_map<mapl_of<P>::value>(t); }
 // thread t's butterfly index base in pass p
 template <class P, int p>
 __device__ __forceinline__ int tpass(int t) {
-  if constexpr (p == 0 || p == P::NP - 1) return tmap<P>(t);
+  if constexpr (p == P::NP - 1) return tmapl<P>(t);
+  else if constexpr (p == 0) return tmap0<P>(t);
   else return t;
 }
 
-template <class P>
-struct Swz : P {
-  static_assert(P::TF % 64 == 0 && (P::N / P::R[0]) % 32 == 0, "sigma permutes 32-lane runs");
-  static constexpr int PADSH = 5;
-  static constexpr bool SIGMA = true;
-  static constexpr int LDS = P::N + P::N / 32;
+// A plan with its exchange geometry set (see above).
+template <class P, int M0, int ML, int S = 5>
+struct Lanes : P {
+  static_assert(M0 != kMapPair || P::TF == 64, "the pair map is for one-wave frames");
+  static_assert(P::TF % 64 == 0 && (P::N / P::R[0]) % 32 == 0, "maps permute 32-lane runs");
+  static constexpr int PADSH = S;
+  static constexpr int MAP0 = M0;
+  static constexpr int MAPL = ML;
+  static constexpr int LDS = P::N + (P::N >> S);
 };
+template <class P>
+using Swz = Lanes<P, kMapSigma, kMapSigma, 5>;
 
 // A plan whose frame is owned by one wave and whose LDS slice is private to
 // that wave: the engine's exchanges then need only a wave barrier (LDS
@@ -708,12 +733,12 @@ __device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW t
 template <class P>
 __device__ __forceinline__ int in_index(int t, int e) {          // pass-0 operand e of thread t
   constexpr int R = P::R[0];
-  return tmap<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
+  return tmap0<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
 }
 template <class P>
 __device__ __forceinline__ int out_index(int t, int e) {         // result e of thread t
   constexpr int R = P::RL;
-  return tmap<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
+  return tmapl<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
 }
 
 // ---------------------------------------------------------------------------
@@ -741,7 +766,10 @@ using Plan256d = Plan<256, 4, 4, 4, 4, 4>;
 // Polyphase front of the D = 4 decimating FIR: the two radix-16 passes of a
 // 1024-point transform = the 256-point spectra of its 4 polyphase components
 // (pass-1 twiddles = Plan256's table).
-using Plan1024q = Partial<Plan<1024, 16, 16, 16>>;
+using Plan1024q = Lanes<Partial<Plan<1024, 16, 16, 16>>, kMapPair, kMapId>;
+// The D = 1 FIR's one-wave overlap-save plan with the pair map in its first and
+// last pass (16-byte segment loads, conflict-free exchanges).
+using Plan1024x = Lanes<Plan1024s, kMapPair, kMapPair>;
 // The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
 using Plan8192x = Swz<Plan8192>;
 

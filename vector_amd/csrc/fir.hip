@@ -44,7 +44,7 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 // Two consecutive blocks per workgroup (fft_pair: the LDS stores of one
 // segment overlap the other's butterflies), twiddles from register anchors.
 // MIX: the NCO mixer applied to every loaded sample (vsig_fir_exec_mix_dev).
-template <class P, bool MIX = false>
+template <class P, bool MIX = false, bool X4 = false>
 __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
@@ -63,6 +63,9 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
   if constexpr (MIX) {
     load_segment_mix<P>(a, x, g0 + b0 * hop - lo, n, t, mix);
     load_segment_mix<P>(d, x, g0 + b1 * hop - lo, n, t, mix);
+  } else if constexpr (X4) {
+    load_segment_x4<P>(a, x, g0 + b0 * hop - lo, n, t);
+    load_segment_x4<P>(d, x, g0 + b1 * hop - lo, n, t);
   } else {
     load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
     load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
@@ -184,7 +187,7 @@ __device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
 // for the kernel (profiles/r02_v12_ab.txt), i.e. the loads / stores of this
 // access pattern alone run at 5.5 TB/s and the transforms add ~0.45 ms.
 
-template <bool MIX = false>
+template <bool MIX = false, bool X4 = false>
 __global__ __launch_bounds__(64) void fir_poly_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
     long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
@@ -208,6 +211,9 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
   if constexpr (MIX) {
     load_segment_mix<P>(a, x, g0 + (2 * b) * hop - lo2, n, t, mix);
     load_segment_mix<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t, mix);
+  } else if constexpr (X4) {
+    load_segment_x4<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
+    load_segment_x4<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
   } else {
     load_segment<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
     load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
@@ -271,6 +277,15 @@ hipError_t launch_fir_poly_gtable(const float2* Hs, float2* G, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Every segment start x + off + k hop (k >= 0) 16-byte aligned: the 16-byte
+// segment loads (load_segment_x4) apply.
+static bool x4_aligned(const float2* x, long long off, long long hop) {
+#ifdef VSIG_NO_X4       // tuning builds: 8-byte segment loads only
+  return false;
+#endif
+  return (hop % 2) == 0 && ((reinterpret_cast<uintptr_t>(x) + 8 * (uintptr_t)off) & 15) == 0;
+}
+
 hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const float2* G, int lo2,
                            long long hop, float2* y, const float2* tw, const float2* twd,
                            hipStream_t st, const MixArgs* mix) {
@@ -280,6 +295,9 @@ hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const flo
   const MixArgs m = mix ? *mix : MixArgs{};
   if (mix)
     hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+  else if (x4_aligned(x, g0 - lo2, hop))
+    hipLaunchKernelGGL((fir_poly_kernel<false, true>), g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw,
+                       twd, m);
   else
     hipLaunchKernelGGL(fir_poly_kernel<false>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
   return hipGetLastError();
@@ -324,11 +342,18 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
         return;
       }
     }
-      hipLaunchKernelGGL((fir_os_kernel<PL, false>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps,
-                         hop, decim, y, nblocks, tw, m);
+    if constexpr (map0_of<PL>::value == kMapPair) {
+      if (x4_aligned(x, g0 - (ntaps - 1), hop)) {
+        hipLaunchKernelGGL((fir_os_kernel<PL, false, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs,
+                           ntaps, hop, decim, y, nblocks, tw, m);
+        return;
+      }
+    }
+    hipLaunchKernelGGL((fir_os_kernel<PL, false>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps,
+                       hop, decim, y, nblocks, tw, m);
   };
   switch (M) {
-    case 1024: run(Plan1024s{}); break;
+    case 1024: run(Plan1024x{}); break;
     case 4096: if (mix) return hipErrorInvalidValue; run(Plan4096{}); break;
     case 8192: if (mix) return hipErrorInvalidValue; run(Plan8192{}); break;
     case 16384: if (mix) return hipErrorInvalidValue; run(Plan16384{}); break;

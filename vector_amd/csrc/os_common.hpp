@@ -45,6 +45,37 @@ __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict
   }
 }
 
+// load_segment for one-wave plans whose first pass has the pair map (operand
+// e of thread t = x[s0 + m(t) + 64 e], m(l) = 2l for l < 32, 2(l-32) + 1
+// above) by 16-byte loads: load i gives lane l the samples 2l + 128 i and
+// 2l + 1 + 128 i; one v_permlane32_swap of the odd samples of lanes < 32 with
+// the even samples of lanes >= 32 leaves lane l with x[m(l) + 128 i] and
+// x[m(l) + 64 + 128 i], i.e. operands 2 i and 2 i + 1 -- half the load
+// instructions of load_segment (the FIR's load / store pattern measured 8 %
+// faster this way with its transforms knocked out).  x + s0 must be 16-byte
+// aligned (a launch-time property: the callers' segment starts are all even
+// offsets from one base); segments not inside [0, n) take load_segment.
+template <class P>
+__device__ __forceinline__ void load_segment_x4(float2* v, const float2* __restrict__ x,
+                                                long long s0, long long n, int t) {
+  static_assert(map0_of<P>::value == kMapPair && P::TF == 64 && P::E == 16 && P::R[0] == 16,
+                "operand layout m(t) + 64 e");
+  if (s0 >= 0 && s0 + P::N <= n) {
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4* b4 = reinterpret_cast<const f4*>(x + s0);
+#pragma unroll
+    for (int i = 0; i < P::E / 2; ++i) {
+      const f4 u = b4[t + 64 * i];
+      const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(u.x), __float_as_uint(u.z), false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(u.y), __float_as_uint(u.w), false, false);
+      v[2 * i] = make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0]));
+      v[2 * i + 1] = make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+    }
+  } else {
+    load_segment<P>(v, x, s0, n, t);
+  }
+}
+
 // load_segment with the NCO mixer applied to each sample (global index
 // mix.i0 + s0 + i; the zero fill stays zero): one double-precision phase per
 // lane (sample g + t), then the per-element offsets' rotations
@@ -53,9 +84,9 @@ template <class P>
 __device__ __forceinline__ void load_segment_mix(float2* v, const float2* __restrict__ x,
                                                  long long s0, long long n, int t, const MixArgs& mix) {
   static_assert(P::TF == 64 && P::E == 16 && P::R[0] == 16,
-                "the rotation table assumes in_index(t, e) = t + 64 e");
+                "the rotation table assumes in_index(t, e) = m(t) + 64 e");
   load_segment<P>(v, x, s0, n, t);
-  const float2 r0 = mix_rot_fast(mix.i0 + s0 + t, mix.wsr);
+  const float2 r0 = mix_rot_fast(mix.i0 + s0 + tmap0<P>(t), mix.wsr);
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const float2 r = cmul(r0, make_float2(mix.rot[2 * e], mix.rot[2 * e + 1]));
