@@ -232,7 +232,12 @@ __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 //   kMapPair  m(t) = ((t & 31) << 1) | (t >> 5)   (TF = 64: lane l < 32 takes
 //             j = 2l, lane l + 32 takes j = 2l + 1) -- the layout a 16-byte
 //             load (samples 2l, 2l + 1) reaches after one v_permlane32_swap
-//             (load_segment_x4).
+//             (load_segment_x4);
+//   kMapIlv   butterflies j = B t + b (B = E / R per thread: adjacent j), so a
+//             first pass with two butterflies per thread reads its operands
+//             x[2t + b + (N/R) r] as one 16-byte load per r and a last pass
+//             leaves adjacent bins 2t, 2t + 1 in one thread (8-byte |X|^2
+//             pairs) -- no lane exchange at all.
 // Why padding 1 per 32 with sigma or pair maps (Plan8192x, the FIR plans): the
 // first pass's stride-R scatter stores (R j + r, ds_write_b64: 16-lane groups,
 // banks mod 32 dwords) need the padding to differ across the group's j, and
@@ -242,7 +247,7 @@ __device__ __forceinline__ int lpad(int i) { return i + (i >> 4); }
 // per ds_read_b64); 1 per 32 serves the reads, and both maps give each store
 // group 16 j of one parity, whose padding j / 2 is again distinct.  The
 // operand / result layouts follow the maps (in_index: MAP0, out_index: MAPL).
-constexpr int kMapId = 0, kMapSigma = 1, kMapPair = 2;
+constexpr int kMapId = 0, kMapSigma = 1, kMapPair = 2, kMapIlv = 3;
 template <class P, class = void>
 struct padsh_of { static constexpr int value = 4; };
 template <class P>
@@ -268,18 +273,29 @@ template <class P>
 __device__ __forceinline__ int tmap0(int t) { return lane_map<map0_of<P>::value>(t); }
 template <class P>
 __device__ __forceinline__ int tmapl(int t) { return lane_map<mapl_of<P>::value>(t); }
-// thread t's butterfly index base in pass p
+template <class P, int p>
+constexpr int pass_map() {
+  return p == P::NP - 1 ? mapl_of<P>::value : p == 0 ? map0_of<P>::value : kMapId;
+}
+// thread t's butterfly index base in pass p (maps other than kMapIlv)
 template <class P, int p>
 __device__ __forceinline__ int tpass(int t) {
-  if constexpr (p == P::NP - 1) return tmapl<P>(t);
-  else if constexpr (p == 0) return tmap0<P>(t);
-  else return t;
+  static_assert(pass_map<P, p>() != kMapIlv, "kMapIlv: use bfly");
+  return lane_map<pass_map<P, p>()>(t);
+}
+// butterfly b of thread t in pass p
+template <class P, int p>
+__device__ __forceinline__ int bfly(int t, int b) {
+  if constexpr (pass_map<P, p>() == kMapIlv) return (P::E / P::R[p]) * t + b;
+  else return lane_map<pass_map<P, p>()>(t) + b * P::TF;
 }
 
 // A plan with its exchange geometry set (see above).
 template <class P, int M0, int ML, int S = 5>
 struct Lanes : P {
   static_assert(M0 != kMapPair || P::TF == 64, "the pair map is for one-wave frames");
+  static_assert((M0 != kMapIlv || P::E / P::R[0] == 2) && (ML != kMapIlv || P::E / P::RL == 2),
+                "the interleaved map pairs two butterflies per thread");
   static_assert(P::TF % 64 == 0 && (P::N / P::R[0]) % 32 == 0, "maps permute 32-lane runs");
   static constexpr int PADSH = S;
   static constexpr int MAP0 = M0;
@@ -397,7 +413,7 @@ __device__ __forceinline__ void load_rtw(float2* w, const float2* __restrict__ t
     constexpr int R = P::R[p], Ns = P::ns(p), NB = rtw_nb<P>(p);
     static_for<0, NB>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
-      const int k = (tpass<P, p>(t) + b * P::TF) & (Ns - 1);
+      const int k = bfly<P, p>(t, b) & (Ns - 1);
 #pragma unroll
       for (int r = 1; r < R; ++r) w[rtw_off<P>(p) + b * (R - 1) + r - 1] = tw[P::twoff(p) + (r - 1) * Ns + k];
     });
@@ -423,7 +439,7 @@ __device__ __forceinline__ void load_anchors(float2* wa, const float2* __restric
     constexpr int R = P::R[p], Ns = P::ns(p), B = P::E / R, NA = nanch<P>(p);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
-      const int k = (tpass<P, p>(t) + b * P::TF) & (Ns - 1);
+      const int k = bfly<P, p>(t, b) & (Ns - 1);
       static_for<0, NA>([&](auto ai) {
         constexpr int a = decltype(ai)::value;
         constexpr int r = a == 0 ? 1 : 8 * a;
@@ -444,7 +460,7 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
   if constexpr (std::is_same<TW, TwTable>::value) {
-    const unsigned j = (unsigned)tpass<P, p>(t) + b * P::TF;
+    const unsigned j = (unsigned)bfly<P, p>(t, b);
     const unsigned k = j & (Ns - 1);
     const float2* twp = tws.tw + P::twoff(p);
 #pragma unroll
@@ -457,7 +473,7 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
   } else if constexpr (std::is_same<TW, TwLds>::value) {
     constexpr int S = tw2_shift<P>();
     constexpr int stride = P::N / (Ns * R);       // W_{Ns R}^{rk} = W_N^{rk stride}
-    const int j = tpass<P, p>(t) + b * P::TF;
+    const int j = bfly<P, p>(t, b);
     const int k = j & (Ns - 1);
     const float2* A = tws.t2;
     const float2* Bt = tws.t2 + tw2_hi<P>();
@@ -538,7 +554,7 @@ __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
   constexpr int B = P::E / R;
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
-    const int j = tpass<P, p>(t) + b * P::TF;
+    const int j = bfly<P, p>(t, b);
     const int bp = store_base<P, p>(j);
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
@@ -552,15 +568,27 @@ template <class P, int p>
 __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
-  const int tl = tpass<P, p>(t);
-  const int tp = lpadp<P>(tl);
-  static_for<0, B>([&](auto bi) {
-    constexpr int b = decltype(bi)::value;
-    static_for<0, R>([&](auto ri) {
-      constexpr int r = decltype(ri)::value;
-      v[b * R + r] = lds[lpad_off<P, b * P::TF + r * (P::N / R)>(tl, tp)];
+  if constexpr (pass_map<P, p>() == kMapIlv) {
+    static_for<0, B>([&](auto bi) {
+      constexpr int b = decltype(bi)::value;
+      const int jb = bfly<P, p>(t, b);
+      const int jp = lpadp<P>(jb);
+      static_for<0, R>([&](auto ri) {
+        constexpr int r = decltype(ri)::value;
+        v[b * R + r] = lds[lpad_off<P, r * (P::N / R)>(jb, jp)];
+      });
     });
-  });
+  } else {
+    const int tl = tpass<P, p>(t);
+    const int tp = lpadp<P>(tl);
+    static_for<0, B>([&](auto bi) {
+      constexpr int b = decltype(bi)::value;
+      static_for<0, R>([&](auto ri) {
+        constexpr int r = decltype(ri)::value;
+        v[b * R + r] = lds[lpad_off<P, b * P::TF + r * (P::N / R)>(tl, tp)];
+      });
+    });
+  }
 }
 
 // Split exchange: real and imaginary parts go through an LDS buffer of N
@@ -573,7 +601,7 @@ __device__ __forceinline__ void fft_store_c(const float2* v, float* lds, int t) 
   constexpr int B = P::E / R;
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
-    const int j = tpass<P, p>(t) + b * P::TF;
+    const int j = bfly<P, p>(t, b);
     const int bp = store_base<P, p>(j);
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
@@ -587,6 +615,7 @@ template <class P, int p, int C>
 __device__ __forceinline__ void fft_load_c(float2* v, const float* lds, int t) {
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
+  static_assert(pass_map<P, p>() != kMapIlv, "split exchange: plain maps only");
   const int tl = tpass<P, p>(t);
   const int tp = lpadp<P>(tl);
   static_for<0, B>([&](auto bi) {
@@ -733,12 +762,12 @@ __device__ __forceinline__ void fft_pair(float2* a, float2* d, float2* lds, TW t
 template <class P>
 __device__ __forceinline__ int in_index(int t, int e) {          // pass-0 operand e of thread t
   constexpr int R = P::R[0];
-  return tmap0<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
+  return bfly<P, 0>(t, e / R) + (e % R) * (P::N / R);
 }
 template <class P>
 __device__ __forceinline__ int out_index(int t, int e) {         // result e of thread t
   constexpr int R = P::RL;
-  return tmapl<P>(t) + (e / R) * P::TF + (e % R) * (P::N / R);
+  return bfly<P, P::NP - 1>(t, e / R) + (e % R) * (P::N / R);
 }
 
 // ---------------------------------------------------------------------------
@@ -772,6 +801,9 @@ using Plan1024q = Lanes<Partial<Plan<1024, 16, 16, 16>>, kMapPair, kMapId>;
 using Plan1024x = Lanes<Plan1024s, kMapPair, kMapPair>;
 // The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
 using Plan8192x = Swz<Plan8192>;
+// The PSD's 8192-point plan with interleaved first / last passes (16-byte
+// frame loads, 8-byte |X|^2 stores, conflict-free exchanges).
+using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, 5>;
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

@@ -33,6 +33,36 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
   }
 }
 
+// The same for decim = 1 with the pair lane map (out_index(t, e) = m(t) + 64 e)
+// by 16-byte stores: the inverse of load_segment_x4's swap gives lane l the
+// outputs 2l + 128 i and 2l + 1 + 128 i.  Needs lo even and y + b hop 16-byte
+// aligned (launch-time choice); an odd tail (lim odd) stores its last single.
+template <class P>
+__device__ __forceinline__ void fir_store_x4(const float2* v, float2* __restrict__ y, long long b,
+                                             long long hop, int lo, long long nloc, int t) {
+  static_assert(mapl_of<P>::value == kMapPair && P::TF == 64 && P::E == 16 && P::RL == 16,
+                "result layout m(t) + 64 e");
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const long long gb = b * hop;
+  const long long rem = nloc - gb;
+  const int lim = rem < hop ? (int)rem : (int)hop;
+  float2* yb = y + gb;
+#pragma unroll
+  for (int i = 0; i < P::E / 2; ++i) {
+    const float2 p = cconj(v[2 * i]), q = cconj(v[2 * i + 1]);
+    const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(p.x), __float_as_uint(q.x), false, false);
+    const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(p.y), __float_as_uint(q.y), false, false);
+    const int io = 2 * t + 128 * i - lo;               // even: lo is
+    const f4 w = {__uint_as_float(rx[0]), __uint_as_float(ry[0]), __uint_as_float(rx[1]),
+                  __uint_as_float(ry[1])};
+    if (io >= 0 && io + 1 < lim) {
+      __builtin_nontemporal_store(w, reinterpret_cast<f4*>(yb + io));
+    } else if (io >= 0 && io < lim) {
+      st_stream(yb + io, make_float2(w.x, w.y));
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // FIR, overlap-save.  Block b produces outputs g in [b*hop, b*hop + hop) of
 //   y[g] = sum_{m < ntaps} h[m] x[g0 + g - m]   (x = 0 outside [0, n))
@@ -44,7 +74,7 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 // Two consecutive blocks per workgroup (fft_pair: the LDS stores of one
 // segment overlap the other's butterflies), twiddles from register anchors.
 // MIX: the NCO mixer applied to every loaded sample (vsig_fir_exec_mix_dev).
-template <class P, bool MIX = false, bool X4 = false>
+template <class P, bool MIX = false, bool X4 = false, bool XS = false>
 __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
@@ -80,8 +110,13 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
   }
   launder_anchors<P>(wa);
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
-  fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
-  fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
+  if constexpr (XS) {
+    fir_store_x4<P>(a, y, b0, hop, lo, nloc, t);
+    fir_store_x4<P>(d, y, b1, hop, lo, nloc, t);
+  } else {
+    fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
+    fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -343,9 +378,18 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
       }
     }
     if constexpr (map0_of<PL>::value == kMapPair) {
+#ifdef VSIG_NO_XS      // tuning builds: 8-byte stores
+      const bool xs = false;
+#else
+      const bool xs = decim == 1 && (ntaps - 1) % 2 == 0 && x4_aligned(y, 0, hop);
+#endif
       if (x4_aligned(x, g0 - (ntaps - 1), hop)) {
-        hipLaunchKernelGGL((fir_os_kernel<PL, false, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs,
-                           ntaps, hop, decim, y, nblocks, tw, m);
+        if (xs)
+          hipLaunchKernelGGL((fir_os_kernel<PL, false, true, true>), grid, dim3(PL::TF), 0, st, x, n, g0,
+                             Hs, ntaps, hop, decim, y, nblocks, tw, m);
+        else
+          hipLaunchKernelGGL((fir_os_kernel<PL, false, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs,
+                             ntaps, hop, decim, y, nblocks, tw, m);
         return;
       }
     }

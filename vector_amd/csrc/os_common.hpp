@@ -86,7 +86,7 @@ __device__ __forceinline__ void load_segment_mix(float2* v, const float2* __rest
   static_assert(P::TF == 64 && P::E == 16 && P::R[0] == 16,
                 "the rotation table assumes in_index(t, e) = m(t) + 64 e");
   load_segment<P>(v, x, s0, n, t);
-  const float2 r0 = mix_rot_fast(mix.i0 + s0 + tmap0<P>(t), mix.wsr);
+  const float2 r0 = mix_rot_fast(mix.i0 + s0 + in_index<P>(t, 0), mix.wsr);
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const float2 r = cmul(r0, make_float2(mix.rot[2 * e], mix.rot[2 * e + 1]));

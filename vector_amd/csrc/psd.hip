@@ -31,7 +31,7 @@ template <class P>
 __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
     const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
-    const float2* __restrict__ tw) {
+    const float2* __restrict__ tw, bool x4) {
   static_assert(P::TF >= 256, "one frame per block");
   __shared__ float2 lds[P::LDS];
   const int t = threadIdx.x;
@@ -39,14 +39,43 @@ __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
   float2 v[2][P::E];
+  constexpr bool ILV = map0_of<P>::value == kMapIlv && mapl_of<P>::value == kMapIlv;
+  // interleaved plans (Plan8192i): thread t's operands are x[2t + b + (N/R0) r],
+  // b < 2 -- one 16-byte load per r -- when the frames are contiguous, full
+  // and 16-byte aligned (uniform per launch: stride 1, nperseg = N, even hop,
+  // aligned x; the caller's flag x4)
+  if constexpr (ILV) {
+    static_assert(P::E == 2 * P::R[0] && P::E == 2 * P::RL, "two butterflies per thread");
+    if (x4) {
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      constexpr int R0 = P::R[0], S0 = P::N / R0;
 #pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    psd_load<P>(v[f], x, stride, nperseg, hop, u * 2 + f, nframes, t);
+      for (int f = 0; f < 2; ++f) {
+        const long long frame = u * 2 + f;
+        const bool active = frame < nframes;
+        const float2* xf = x + (active ? frame * hop : 0);
 #pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const int i = in_index<P>(t, e);
-      const float w = i < nperseg ? win[i] : 0.f;
-      v[f][e] = make_float2(v[f][e].x * w, v[f][e].y * w);
+        for (int r = 0; r < R0; ++r) {
+          const int i = 2 * t + S0 * r;
+          const f4 q = active ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(xf + i))
+                              : f4{0.f, 0.f, 0.f, 0.f};
+          const float2 w2 = *reinterpret_cast<const float2*>(win + i);
+          v[f][r] = make_float2(q.x * w2.x, q.y * w2.x);
+          v[f][R0 + r] = make_float2(q.z * w2.y, q.w * w2.y);
+        }
+      }
+    }
+  }
+  if (!ILV || !x4) {
+#pragma unroll
+    for (int f = 0; f < 2; ++f) {
+      psd_load<P>(v[f], x, stride, nperseg, hop, u * 2 + f, nframes, t);
+#pragma unroll
+      for (int e = 0; e < P::E; ++e) {
+        const int i = in_index<P>(t, e);
+        const float w = i < nperseg ? win[i] : 0.f;
+        v[f][e] = make_float2(v[f][e].x * w, v[f][e].y * w);
+      }
     }
   }
   launder_anchors<P>(wa);
@@ -56,11 +85,26 @@ __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
     const long long frame = u * 2 + f;
     if (frame < nframes) {
       float* of = out + frame * P::N;
+      if constexpr (ILV) {
+        // bins 2t + RLs r and the next one: one 8-byte store each (fftshift by
+        // N/2 keeps the pair adjacent)
+        typedef float f2 __attribute__((ext_vector_type(2)));
+        constexpr int RL = P::RL, SL = P::N / RL;
 #pragma unroll
-      for (int e = 0; e < P::E; ++e) {
-        const int i = out_index<P>(t, e);
-        const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
-        __builtin_nontemporal_store((v[f][e].x * v[f][e].x + v[f][e].y * v[f][e].y) * scale, of + o);
+        for (int r = 0; r < RL; ++r) {
+          const int i = 2 * t + SL * r;
+          const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+          const float2 a0 = v[f][r], a1 = v[f][RL + r];
+          const f2 pw = {(a0.x * a0.x + a0.y * a0.y) * scale, (a1.x * a1.x + a1.y * a1.y) * scale};
+          __builtin_nontemporal_store(pw, reinterpret_cast<f2*>(of + o));
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < P::E; ++e) {
+          const int i = out_index<P>(t, e);
+          const int o = shift ? ((i + P::N / 2) & (P::N - 1)) : i;
+          __builtin_nontemporal_store((v[f][e].x * v[f][e].x + v[f][e].y * v[f][e].y) * scale, of + o);
+        }
       }
     }
   }
@@ -231,10 +275,19 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                       long long hop, float scale, float* out, long long nframes, int shift,
                       const float2* tw, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
+#ifndef VSIG_NO_ILV
+  if (N == 8192) {      // interleaved first / last pass: 16-byte loads, 8-byte stores
+    const bool x4 = stride == 1 && nperseg == N && hop % 2 == 0 &&
+                    (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(win) & 7) == 0;
+    hipLaunchKernelGGL(psd_pair_kernel<Plan8192i>, dim3((unsigned)((nframes + 1) / 2)), dim3(Plan8192i::TF),
+                       0, st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, x4);
+    return hipGetLastError();
+  }
+#endif
   VSIG_PLAN_SWITCH(N, {
     if constexpr (PL::TF >= 256) {
       hipLaunchKernelGGL(psd_pair_kernel<PL>, dim3((unsigned)((nframes + 1) / 2)), dim3(PL::TF), 0,
-                         st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw);
+                         st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, false);
     } else {
       constexpr int FPB = block_threads<PL>() / PL::TF;
       hipLaunchKernelGGL(psd_split_kernel<PL>, dim3((unsigned)((nframes + FPB - 1) / FPB)),

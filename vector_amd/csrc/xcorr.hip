@@ -243,7 +243,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   };
   float2 a[P::E], d[P::E];
   load_halves<P>(a, d, s, b * hop - off, n, t);
-  const float2 w = wt[tmap0<P>(t)];      // W_M^j, j = in_index(t, 0)
+  const float2 w = wt[in_index<P>(t, 0)];      // W_M^j, j = in_index(t, 0)
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 x0 = a[e], x1 = d[e];
