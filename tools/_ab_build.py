@@ -11,7 +11,7 @@ VARIANTS = {
     "libvsig_fold": ("VSIG_FIR_DEC_FOLD",),
     "libvsig_firko": ("VSIG_FIR_KO",),
     "libvsig_nox4": ("VSIG_NO_X4",),
-    "libvsig_noilv": ("VSIG_NO_ILV",),
+    "libvsig_xilv": ("VSIG_XCORR_ILV",),
     "libvsig_pfb128": ("VSIG_PFB_FPG=128",),
     "libvsig_pfb256": ("VSIG_PFB_FPG=256",),
     "libvsig_pfb512": ("VSIG_PFB_FPG=512",),

@@ -114,7 +114,8 @@ struct RefineGeom {
   int rev;              // raw (kernel) index -> final: nout - 1 - raw
   int from_array;       // items are 64-output chunks of a stored array
   long long hop;        // partial items: outputs per block, waves per block,
-  int waves, Q, stride; //   rows per item and their stride
+  int waves, Q, stride; //   rows per item and their stride,
+  int wstep, rsub;      //   wave base step, 64-output rows per stride step
 };
 
 __device__ __forceinline__ long long item_output(const RefineGeom& g, long long item, int q, int l) {
@@ -128,7 +129,7 @@ __device__ __forceinline__ long long item_output(const RefineGeom& g, long long 
   const long long ob = b * g.hop;
   const long long rem = g.nout - ob;
   const long long lim = rem < g.hop ? rem : g.hop;
-  const long long r = 64LL * w + l + (long long)g.stride * q;
+  const long long r = (long long)g.wstep * w + l + 64LL * (q % g.rsub) + (long long)g.stride * (q / g.rsub);
   if (r >= lim) return -1;
   raw = ob + r;
   return g.rev ? g.nout - 1 - raw : raw;
@@ -336,7 +337,8 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   double2* cv = reinterpret_cast<double2*>(oidx + n);
   hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
   if (e != hipSuccess) return e;
-  RefineGeom g{r.nout, r.F, r.na, r.nv, r.rev, r.from_array, r.hop, r.waves, r.Q, r.stride};
+  RefineGeom g{r.nout, r.F, r.na, r.nv, r.rev, r.from_array, r.hop, r.waves, r.Q, r.stride,
+               r.wstep, r.rsub};
   PeakPartial* rec = r.rec;
   if (r.from_array) {
     const long long grid = (r.nout + 255) / 256;

@@ -277,12 +277,13 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
   r.nout = nout; r.F = op.F; r.rev = rev;
   if (c64) {
     r.from_array = 1; r.c64 = c64; r.Q = 1; r.stride = 0; r.waves = 1; r.hop = 64;
+    r.wstep = 64; r.rsub = 1;
   } else {
-    int waves, Q, stride, plan;
-    if (vsig::xcorr_geom(M, &waves, &Q, &stride, &plan) != hipSuccess)
+    int waves, Q, stride, plan, wstep, rsub;
+    if (vsig::xcorr_geom(M, &waves, &Q, &stride, &plan, &wstep, &rsub) != hipSuccess)
       return fail(c, VSIG_E_INVALID, "refine: no correlator geometry for M");
     r.parts = c->partials; r.nparts = nparts; r.hop = hop;
-    r.waves = waves; r.Q = Q; r.stride = stride;
+    r.waves = waves; r.Q = Q; r.stride = stride; r.wstep = wstep; r.rsub = rsub;
   }
   r.eps = c->refine_eps_ppm * 1e-6;
   r.eps2 = 1e-6;
@@ -846,10 +847,13 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
   vsig_ctx* c = x->ctx;
   PeakPartial* rec = peak_dev ? reinterpret_cast<PeakPartial*>(peak_dev) : c->result;
   if (x->Ps.size() == 1 && x->L <= (x->M == 32768 ? 16384 : 8192)) {
-    const long long hop = (long long)x->M - x->L + 1;
+    // outputs per block: M - L + 1, rounded down to even at M = 16384 (every
+    // segment start then has one parity: the correlator's 16-byte loads)
+    long long hop = (long long)x->M - x->L + 1;
+    if (x->M == 16384 && hop > 1) hop &= ~1LL;
     const long long nblocks = (nout + hop - 1) / hop;
-    int waves, Q, stride, plan;
-    if (vsig::xcorr_geom(x->M, &waves, &Q, &stride, &plan) != hipSuccess)
+    int waves, Q, stride, plan, wstep, rsub;
+    if (vsig::xcorr_geom(x->M, &waves, &Q, &stride, &plan, &wstep, &rsub) != hipSuccess)
       return fail(c, VSIG_E_UNSUPPORTED, "correlator block size");
     const long long nparts = nblocks * waves;   // one partial per wave
     int rc = ensure_partials(c, nparts);
@@ -857,7 +861,7 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     const float2* tw;
     const float2* wt = nullptr;
     if ((rc = get_twiddles(c, plan, &tw))) return rc;
-    if (x->M >= 16384 && (rc = get_half_tw(c, x->M, x->M == 16384 ? 256 : 1024, &wt))) return rc;
+    if (x->M >= 16384 && (rc = get_half_tw(c, x->M, x->M == 16384 ? 512 : 1024, &wt))) return rc;
     {
       Timed t(c, "xcorr");
       HIPCHK(c, vsig::launch_xcorr_os(x->M, s, n, x->Ps[0], off, nout, hop, cout, store_mode,
@@ -877,7 +881,7 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     cbuf = static_cast<float2*>(x->cbuf);
   }
   const float2 *tw, *wt;
-  if ((rc = get_twiddles(c, 8192, &tw)) || (rc = get_half_tw(c, M, 256, &wt))) return rc;
+  if ((rc = get_twiddles(c, 8192, &tw)) || (rc = get_half_tw(c, M, 512, &wt))) return rc;
   {
     Timed t(c, "xcorr");            // the whole chunked correlation + its peak pass
     for (size_t p = 0; p < x->Ps.size(); ++p) {

@@ -117,12 +117,14 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
                          int ntaps, long long hop, int decim, float2* y, const float2* tw,
                          hipStream_t st, const MixArgs* mix = nullptr);
 // Correlator, M in {4096, 8192, 16384} (16384: half-frame kernel, tw = the
-// 8192-point table, wt = W_M^t for t < 256).
+// 8192-point table, wt = W_M^t for t < 512).
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, const float2* wt,
                            hipStream_t st);
-hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan);
+// Outputs of wave w of block b of the correlator for M (the refine pass's
+// items): ob + wstep w + l + 64 (q % rsub) + stride (q / rsub), l < 64, q < Q.
+hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* wstep, int* rsub);
 #ifdef VSIG_TUNING
 // Tuning micro-benchmarks: iters FFTs per frame, frames blocks (key: plan key).
 hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const float2* tw, int twl,
@@ -147,7 +149,8 @@ struct RefineArgs {
   const float2* c64;
   const PeakPartial* parts;         // or from the fused correlator's wave partials
   long long nparts, hop;
-  int waves, Q, stride;             // wave w of block b: ob + 64 w + l + stride q
+  int waves, Q, stride;             // wave w of block b: ob + wstep w + l + 64 (q % rsub)
+  int wstep, rsub;                  //   + stride (q / rsub), l < 64, q < Q (xcorr_geom)
   double eps, eps2;                 // fp32 band, stage-2 band (relative)
   long long cap_items;
   void* scratch;                    // refine_scratch_bytes(cap_items, Q)

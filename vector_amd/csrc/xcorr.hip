@@ -20,7 +20,8 @@ namespace vsig {
 // sum of template chunks).
 // Partials: one per wave.  Wave w of block b covers the outputs
 //   b*hop + 64 w + l + TF q,   l < 64, q < Q   (Q = E, or 2 E for the half
-// kernel), which refine.hip uses to revisit a wave's outputs.
+// kernel; the interleaved half kernel: b*hop + 128 w + [0, 128) + 512 q'),
+// which refine.hip uses to revisit a wave's outputs (xcorr_geom).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void put_c(float2* p, float2 v, bool accum) {
   *p = accum ? cadd(*p, v) : v;
@@ -114,9 +115,12 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
 // block's loads / barriers / LDS exchanges overlap the other's butterflies.
 // The two halves go through fft_pair (LDS stores of one half overlap the
 // other's butterflies), twiddles from register anchors.
-// With P palindromic, in_index == out_index = t + (e / R0) TF + (e % R0) N / R0,
-// so W_M^j = W_M^t * W_64^K(e): one per-thread twiddle (table wt) and a
-// compile-time 64th root per element.
+// With P palindromic, in_index == out_index, and W_M^j = W_M^base * W_64^K(e)
+// (half_root): per-thread twiddles from the table wt (one, or two for the
+// interleaved map whose thread holds j = 2t and 2t + 1) and a compile-time 64th
+// root per element.  The interleaved plan (Plan8192i, tuning builds) reads each
+// half with 16-byte loads when every segment start is 16-byte aligned (hop
+// even: the API rounds M - L + 1 down to even at M = 16384).
 // ---------------------------------------------------------------------------
 // The M = 32768 correlator (templates of 8193 .. 16384 samples in one pass):
 // 16384-point halves, 512 threads x 32 values, 3 passes, one block per CU.
@@ -124,22 +128,54 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
 // per 2^28 samples against 1.42 ms for the M = 16384 kernel (r02_v6 A/B), so
 // shorter templates keep M = 16384.
 using PlanX32k = Plan16384w;
-#ifndef VSIG_NO_SWZ
-using PlanX16k = Plan8192x;     // conflict-free exchanges (fft_engine.hpp Swz)
-#else
+// Default: the sigma map (conflict-free exchanges, 8-byte loads).  The
+// interleaved map (16-byte loads, two split twiddles per thread; tuning build
+// VSIG_XCORR_ILV) measured slower here: 2.67 vs 2.58 ms at config 5, 1.316 vs
+// 1.277 at config 2 (profiles/r02_v19_ab.txt).
+#if defined(VSIG_NO_SWZ)
 using PlanX16k = Plan8192;
+#elif defined(VSIG_XCORR_ILV)
+using PlanX16k = Plan8192i;
+#else
+using PlanX16k = Plan8192x;
 #endif
 
+// in_index(t, e) = base(t, b) + off(e), b = e / R0: the split twiddle
+// W_M^in_index = W_M^base * W_64^half_root(e).  Plain / sigma maps: one base
+// per thread (b's TF step is in off); the interleaved map: base 2t + b (two
+// per-thread twiddles), off = (e % R0) N / R0.
+template <class P>
+constexpr bool plan_ilv() { return map0_of<P>::value == kMapIlv; }
 template <class P, int M>
 constexpr int half_root(int e) {
-  return ((e / P::R[0]) * P::TF + (e % P::R[0]) * (P::N / P::R[0])) / (M / 64);
+  return plan_ilv<P>() ? ((e % P::R[0]) * (P::N / P::R[0])) / (M / 64)
+                       : ((e / P::R[0]) * P::TF + (e % P::R[0]) * (P::N / P::R[0])) / (M / 64);
 }
 
 template <class P>
 __device__ __forceinline__ void load_halves(float2* a, float2* d, const float2* __restrict__ x,
-                                            long long s0, long long n, int t) {
+                                            long long s0, long long n, int t, bool x4) {
   constexpr int H = P::N;
   const float2* base = x + s0;
+  if constexpr (plan_ilv<P>()) {
+    // interleaved operands x[2t + b + (N/R0) r]: one 16-byte load per r and half
+    // (x + s0 16-byte aligned: the launch's x4)
+    constexpr int R0 = P::R[0], S0 = P::N / R0;
+    static_assert(P::E == 2 * R0, "two butterflies per thread");
+    if (x4 && s0 >= 0 && s0 + 2 * H <= n) {
+      typedef float f4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+      for (int r = 0; r < R0; ++r) {
+        const f4 p = *reinterpret_cast<const f4*>(base + 2 * t + S0 * r);
+        const f4 q = *reinterpret_cast<const f4*>(base + H + 2 * t + S0 * r);
+        a[r] = make_float2(p.x, p.y);
+        a[R0 + r] = make_float2(p.z, p.w);
+        d[r] = make_float2(q.x, q.y);
+        d[R0 + r] = make_float2(q.z, q.w);
+      }
+      return;
+    }
+  }
   if (s0 >= 0 && s0 + 2 * H <= n) {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
@@ -226,7 +262,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw,
-    const float2* __restrict__ wt) {
+    const float2* __restrict__ wt, bool x4) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   constexpr int M = 2 * P::N;
   static_assert(P::TF % (M / 64) == 0 && (P::N / P::R[0]) % (M / 64) == 0,
@@ -242,13 +278,15 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
     fft_pair<P>(x, y, lds, TwAnchors{wa}, t);
   };
   float2 a[P::E], d[P::E];
-  load_halves<P>(a, d, s, b * hop - off, n, t);
-  const float2 w = wt[in_index<P>(t, 0)];      // W_M^j, j = in_index(t, 0)
+  load_halves<P>(a, d, s, b * hop - off, n, t, x4);
+  // W_M^base: base = in_index(t, 0) (and in_index(t, R0) for the interleaved map)
+  const float2 w = wt[in_index<P>(t, 0)];
+  const float2 w1 = plan_ilv<P>() ? wt[in_index<P>(t, P::R[0])] : w;
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 x0 = a[e], x1 = d[e];
     a[e] = cadd(x0, x1);
-    d[e] = twc<half_root<P, M>(e), 64>(cmul(csub(x0, x1), w));
+    d[e] = twc<half_root<P, M>(e), 64>(cmul(csub(x0, x1), (plan_ilv<P>() && e >= P::R[0]) ? w1 : w));
   });
   fft2(a, d);
 #pragma unroll
@@ -260,7 +298,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   fft2(a, d);
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
-    const float2 o = twc<half_root<P, M>(e), 64>(cmul(d[e], w));
+    const float2 o = twc<half_root<P, M>(e), 64>(cmul(d[e], (plan_ilv<P>() && e >= P::R[0]) ? w1 : w));
     const float2 ev = a[e];
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
@@ -275,15 +313,17 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (nout <= 0) return hipSuccess;
   const long long nblocks = (nout + hop - 1) / hop;
   if (M == 16384) {
+    // every segment start s - off + b hop 16-byte aligned: 16-byte loads
+    const bool x4 = hop % 2 == 0 && ((reinterpret_cast<uintptr_t>(s) - 8 * (uintptr_t)off) & 15) == 0;
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt);
+                       partials, nblocks, tw, wt, x4);
     return hipGetLastError();
   }
   if (M == 32768) {     // 16384-point halves, one block per CU
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX32k>, dim3((unsigned)nblocks), dim3(PlanX32k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt);
+                       partials, nblocks, tw, wt, false);
     return hipGetLastError();
   }
   auto run = [&](auto plan) {
@@ -301,8 +341,17 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
 
 // Wave geometry of the correlator's partials (see the header comment):
 // waves per block, rows Q and their stride; twiddle plan size.
-hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan) {
+hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* wstep, int* rsub) {
+  *wstep = 64;
+  *rsub = 1;
   if (M == 32768) { *waves = PlanX32k::TF / 64; *Q = 2 * PlanX32k::E; *stride = PlanX32k::TF; *plan = -16384; }
+  else if (M == 16384 && plan_ilv<PlanX16k>()) {
+    // thread t holds j = 2t + b + (N/R0) r (+ N for the second half): wave w's
+    // outputs are 128 w + [0, 128) + (N/R0) r + N h -- two 64-output rows per
+    // step of N/R0 (= 512), 2 E rows in all
+    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::N / PlanX16k::R[0];
+    *wstep = 128; *rsub = 2; *plan = 8192;
+  }
   else if (M == 16384) { *waves = Plan8192::TF / 64; *Q = 2 * Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 8192) { *waves = Plan8192::TF / 64; *Q = Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 4096) { *waves = Plan4096::TF / 64; *Q = Plan4096::E; *stride = Plan4096::TF; *plan = 4096; }
