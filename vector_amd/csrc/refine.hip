@@ -135,10 +135,13 @@ __device__ __forceinline__ long long item_output(const RefineGeom& g, long long 
   return g.rev ? g.nout - 1 - raw : raw;
 }
 
-// Stage 1: one block per (item, q) unit; lane l of every wave one output,
-// the 16 waves a sixteenth of the taps each (independent partial sums, loads
-// unrolled 8-deep so the loop is throughput- not latency-bound), combined in
-// LDS.  vals / idx / cv are indexed by u * 64 + l, u = item slot * Q + q.
+// Stage 1: four blocks per (item, q) unit of 64 outputs, 16 outputs each:
+// thread (w, l) of a 16-wave block sums output 16 sub + (l & 15) over tap
+// chunk 4 w + (l >> 4) of 64 (independent partial sums, loads unrolled
+// 8-deep), the 64 chunk sums combined in LDS in chunk order.  (One block of
+// 64 outputs x 16 chunks ran a 32-batch dependent load chain per lane on 64
+// CUs; this is 8 batches on 256.)  vals / idx / cv are indexed by u * 64 + o,
+// u = item slot * Q + q, o the output's place in the unit.
 template <class T>
 __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __restrict__ v,
                                            long long abase, long long k0, long long k1,
@@ -167,6 +170,9 @@ __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __r
 }
 
 constexpr int kS1Waves = 16;
+constexpr int kS1Outs = 16;                         // outputs per block
+constexpr int kS1Chunks = kS1Waves * 64 / kS1Outs;  // tap chunks per output (64)
+constexpr int kS1Split = 64 / kS1Outs;              // blocks per unit (4)
 
 template <class T>
 __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restrict__ a, const T* __restrict__ v,
@@ -179,41 +185,46 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
   if (keys->status || cnt == 0) return;
   const long long nunits = (cnt < cap ? cnt : cap) * g.Q;
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  __shared__ double pr[kS1Waves][64], pi[kS1Waves][64];
-  for (long long u = blockIdx.x; u < nunits; u += gridDim.x) {   // uniform per block
+  const int ol = l & (kS1Outs - 1);                 // output within the block
+  const int ch = w * (64 / kS1Outs) + (l / kS1Outs); // tap chunk
+  __shared__ double pr[kS1Chunks][kS1Outs], pi[kS1Chunks][kS1Outs];
+  for (long long ub = blockIdx.x; ub < nunits * kS1Split; ub += gridDim.x) {   // uniform per block
+    const long long u = ub / kS1Split;
+    const int sub = (int)(ub - u * kS1Split);
     const long long item = items[u / g.Q];
     const int q = (int)(u % g.Q);
-    const long long o = item_output(g, item, q, l);
+    const int po = sub * kS1Outs + ol;              // output's place in the unit (0..63)
+    const long long o = item_output(g, item, q, po);
     double re = 0.0, im = 0.0;
     if (o >= 0) {
       const long long i = g.F + o;
       long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
-      const long long span = (k1 - k0 + kS1Waves - 1) / kS1Waves;   // this wave's share
-      const long long q0 = k0 + w * span;
+      const long long span = (k1 - k0 + kS1Chunks - 1) / kS1Chunks;   // this chunk's share
+      const long long q0 = k0 + ch * span;
       const long long q1 = q0 + span < k1 ? q0 + span : k1;
       if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im);
     }
-    pr[w][l] = re;
-    pi[w][l] = im;
+    pr[ch][ol] = re;
+    pi[ch][ol] = im;
     __syncthreads();
-    if (w == 0) {
+    if (threadIdx.x < kS1Outs) {                    // lanes 0..15 of wave 0: output ol
       re = 0.0;
       im = 0.0;
-#pragma unroll
-      for (int q2 = 0; q2 < kS1Waves; ++q2) { re += pr[q2][l]; im += pi[q2][l]; }
+#pragma unroll 8
+      for (int c = 0; c < kS1Chunks; ++c) { re += pr[c][ol]; im += pi[c][ol]; }
       const double m2 = o >= 0 ? re * re + im * im : -1.0;
-      const long long e = u * 64 + l;
+      const long long e = u * 64 + po;
       vals[e] = m2;
       oidx[e] = o;
       cv[e] = make_double2(re, im);
       double wm = m2;
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
+      for (int off = kS1Outs / 2; off > 0; off >>= 1) {
         const double o2 = __shfl_xor(wm, off);
         wm = o2 > wm ? o2 : wm;
       }
-      if (l == 0 && wm >= 0.0) atomicMax(&keys->max1, (unsigned long long)__double_as_longlong(wm));
+      if (ol == 0 && wm >= 0.0) atomicMax(&keys->max1, (unsigned long long)__double_as_longlong(wm));
     }
     __syncthreads();
   }
@@ -260,7 +271,22 @@ __global__ __launch_bounds__(256) void refine_stage2(const T* __restrict__ a, co
       tap_range(i, g.na, g.nv, k0, k1);
       const long long abase = i - (g.nv - 1);
       double sr = 0.0, cr = 0.0, si = 0.0, ci = 0.0;
-      for (long long k = k0 + l; k < k1; k += 64) {
+      long long k = k0 + l;
+      // four taps' loads in flight per lane (the accumulation order is the
+      // one-tap loop's: same Dot2 result)
+      for (; k + 3 * 64 < k1; k += 4 * 64) {
+        double2 x[4], y[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) { x[j] = ld2<T>(a, abase + k + 64 * j); y[j] = ld2<T>(v, k + 64 * j); }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          dot2_add(sr, cr, x[j].x, y[j].x);
+          dot2_add(sr, cr, x[j].y, y[j].y);
+          dot2_add(si, ci, x[j].y, y[j].x);
+          dot2_add(si, ci, -x[j].x, y[j].y);
+        }
+      }
+      for (; k < k1; k += 64) {
         const double2 x = ld2<T>(a, abase + k);
         const double2 y = ld2<T>(v, k);
         dot2_add(sr, cr, x.x, y.x);
@@ -349,10 +375,10 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
     hipLaunchKernelGGL(refine_select_partials, dim3((unsigned)grid), dim3(256), 0, st, r.parts,
                        r.nparts, rec, r.eps, r.cap_items, items, keys);
   }
-  // stage grids: stage 1 one block per unit (grid-stride), stage 2 one wave
-  // per 64 entries (grid-stride), capped at a few blocks per CU
-  long long units = r.cap_items * r.Q;
-  if (units > 4096) units = 4096;
+  // stage grids: stage 1 kS1Split blocks per unit (grid-stride), stage 2 one
+  // wave per 64 entries (grid-stride), capped at a few blocks per CU
+  long long units = r.cap_items * r.Q * kS1Split;
+  if (units > 8192) units = 8192;
   const unsigned g1 = (unsigned)units;
   long long g2l = (n + 255) / 256;
   if (g2l > 4096) g2l = 4096;
