@@ -11,6 +11,7 @@ VARIANTS = {
     "libvsig_fold": ("VSIG_FIR_DEC_FOLD",),
     "libvsig_firko": ("VSIG_FIR_KO",),
     "libvsig_nox4": ("VSIG_NO_X4",),
+    "libvsig_nokeyed": ("VSIG_NO_KEYED",),
     "libvsig_xilv": ("VSIG_XCORR_ILV",),
     "libvsig_pfb128": ("VSIG_PFB_FPG=128",),
     "libvsig_pfb256": ("VSIG_PFB_FPG=256",),

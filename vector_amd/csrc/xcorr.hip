@@ -194,6 +194,32 @@ __device__ __forceinline__ void load_halves(float2* a, float2* d, const float2* 
   }
 }
 
+// A thread's outputs out_index(t, e) = m(t) + c_e (+ H for the second half)
+// are evenly spaced: c_e = kStep * rank(e), rank a permutation of [0, E), and
+// H = kStep * E, so rank and index convert by one multiply (plain / sigma
+// maps; the interleaved map's c_e = b + (N/R) r are not).
+template <class P>
+struct KeyedRank {
+  static constexpr int c(int e) { return (e / P::RL) * P::TF + (e % P::RL) * (P::N / P::RL); }
+  static constexpr int rank(int e) {
+    int r = 0;
+    for (int q = 0; q < P::E; ++q) r += c(q) < c(e);
+    return r;
+  }
+  static constexpr int kStep = P::TF < P::N / P::RL ? P::TF : P::N / P::RL;
+  static constexpr bool check() {
+    if (mapl_of<P>::value == kMapIlv || 2 * P::E > 64 || P::N != kStep * P::E) return false;
+    for (int e = 0; e < P::E; ++e)
+      if (c(e) != kStep * rank(e)) return false;
+    return true;
+  }
+#ifdef VSIG_NO_KEYED     // tuning builds: the compare-and-select epilogue
+  static constexpr bool ok = false;
+#else
+  static constexpr bool ok = check();
+#endif
+};
+
 // Epilogue of a half-frame block: a holds outputs i = out_index(t, e), d holds
 // i + H; a thread's indices rise through a then d (first-maximum rule as in
 // xcorr_epilogue).
@@ -225,6 +251,57 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     }
   }
   if (!partials) return;
+  if constexpr (KeyedRank<P>::ok) {
+    // Per-thread argmax by key: the bits of |c|^2 (>= 0, so they order as the
+    // floats) with the low 6 mantissa bits replaced by the output's rank in
+    // the thread (rev: reversed), one v_and_or + one max per output instead of
+    // a compare and two selects.  Ties among values equal to 2^-17 relative go
+    // to the lowest index (rev: the highest) -- numpy's first-max rule in the
+    // (reversed) output space; the partial's max is that truncated |c|^2
+    // (<= 2^-17 low).  The refine band (1e-3) and its exact fp64 re-rank are
+    // unaffected; with refine off the peak is the fp32 result within 8e-6.
+    using KR = KeyedRank<P>;
+    const unsigned rx = rev ? 0u : 63u;
+    unsigned key = 0u;
+    bool any = false;
+    float s1 = 0.f, s2 = 0.f;
+    auto acc = [&](float2 v, int i, int rank, auto masked) {
+      const float a2 = v.x * v.x + v.y * v.y;
+      const unsigned k = (__float_as_uint(a2) & ~63u) | ((unsigned)rank ^ rx);
+      if constexpr (decltype(masked)::value) {
+        const bool ok = i < lim;
+        key = ok ? (k > key ? k : key) : key;
+        any |= ok;
+        s1 += ok ? __builtin_amdgcn_sqrtf(a2) : 0.f;
+        s2 += ok ? a2 : 0.f;
+      } else {
+        key = k > key ? k : key;
+        any = true;
+        s1 += __builtin_amdgcn_sqrtf(a2);
+        s2 += a2;
+      }
+    };
+    if (lim > H) {                     // every index of the a half is valid
+      static_for<0, P::E>([&](auto ei) {
+        constexpr int e = decltype(ei)::value;
+        acc(a[e], 0, KR::rank(e), IC<0>{});
+      });
+    } else {
+      static_for<0, P::E>([&](auto ei) {
+        constexpr int e = decltype(ei)::value;
+        acc(a[e], out_index<P>(t, e), KR::rank(e), IC<1>{});
+      });
+    }
+    static_for<0, P::E>([&](auto ei) {
+      constexpr int e = decltype(ei)::value;
+      acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
+    });
+    const int rank = (int)((key & 63u) ^ rx);
+    const int mi = tmapl<P>(t) + KR::kStep * rank;
+    const float m = any ? __uint_as_float(key & ~63u) : -1.f;
+    wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
+    return;
+  }
   float m = -1.f, s1 = 0.f, s2 = 0.f;
   int mi = 0;
   auto acc = [&](float2 v, int i) {
