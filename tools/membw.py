@@ -49,4 +49,9 @@ for v in range(16, 28):
     name = f"probe_u{U}_8B" + ("_ntl" if v & 2 else "") + ("_nts" if v & 1 else "")
     ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
     res[name] = (round(ms, 4), round(16 * n / ms / 1e6, 1))
+for v in range(28, 34):
+    U = (2, 4, 8)[(v - 28) // 2]
+    name = f"read4to1_u{U}" + ("_ntl" if v & 1 else "")
+    ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
+    res[name] = (round(ms, 4), round(10 * n / ms / 1e6, 1))   # 8 B read + 2 B written per sample
 print(json.dumps(res))

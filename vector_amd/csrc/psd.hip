@@ -182,13 +182,13 @@ __global__ __launch_bounds__(block_threads<P>()) void spectrum_prep(
 // per block with no HBM traffic in the loop — the compute/LDS ceiling of a plan.
 // ---------------------------------------------------------------------------
 template <class P, int TWL>
-__global__ __launch_bounds__(os_threads<P>()) void fft_bench_kernel(float2* __restrict__ io,
+__global__ __launch_bounds__(P::TF) void fft_bench_kernel(float2* __restrict__ io,
                                                                     int iters,
                                                                     const float2* __restrict__ tw) {
   __shared__ float2 lds[P::LDS + (TWL ? tw2_size<P>() : 0)];
   const int t = threadIdx.x;
   float2* t2 = lds + P::LDS;
-  if constexpr (TWL) load_tw2<P>(t2, tw, t, os_threads<P>());
+  if constexpr (TWL) load_tw2<P>(t2, tw, t, P::TF);
   float2 v[P::E];
   float2* f = io + (long long)blockIdx.x * P::N;
 #pragma unroll
@@ -256,7 +256,7 @@ hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const fl
 #define VSIG_FB(PL)                                                                          \
   {                                                                                          \
     auto k = twl ? fft_bench_kernel<PL, 1> : fft_bench_kernel<PL, 0>;                         \
-    hipLaunchKernelGGL(k, dim3(frames), dim3(os_threads<PL>()), 0, st, io, iters, tw);        \
+    hipLaunchKernelGGL(k, dim3(frames), dim3(PL::TF), 0, st, io, iters, tw);        \
   }
   switch (key) {
     case -1024: VSIG_FB(Plan1024s) break;

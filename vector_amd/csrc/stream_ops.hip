@@ -230,8 +230,42 @@ __global__ __launch_bounds__(256) void copy_probe_u(const V* __restrict__ x, lon
   }
 }
 
+// Read-mostly form (the D = 4 FIR's 4:1 pattern without its overlap): each
+// thread loads U float4 (2U samples), writes one float2 per 4 samples.
+template <int U, bool NTL>
+__global__ __launch_bounds__(256) void reduce4_probe(const f4v* __restrict__ x, long long n4,
+                                                     f2v* __restrict__ y) {
+  const long long base = ((long long)blockIdx.x * 256) * U + threadIdx.x;
+  f4v v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * 256;
+    v[u] = i < n4 ? (NTL ? __builtin_nontemporal_load(x + i) : x[i]) : f4v{0, 0, 0, 0};
+  }
+#pragma unroll
+  for (int u = 0; u < U; u += 2) {
+    const long long i = ((long long)blockIdx.x * 256) * (U / 2) + threadIdx.x + (long long)(u / 2) * 256;
+    const f4v s = v[u] + v[u + 1];
+    if (i < n4 / 2) y[i] = f2v{s.x + s.z, s.y + s.w};
+  }
+}
+
 hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
                              hipStream_t st) {
+  if (variant >= 28) {      // read-mostly probes: 28 + (U index)*2 + NTL, U = 2, 4, 8
+    const int ui = (variant - 28) / 2, ntl = variant & 1;
+    const long long n4 = n / 2;
+    const int U = ui == 0 ? 2 : ui == 1 ? 4 : 8;
+    const dim3 g((unsigned)((n4 + 256LL * U - 1) / (256LL * U))), b(256);
+    const f4v* x4 = reinterpret_cast<const f4v*>(x);
+    f2v* y2 = reinterpret_cast<f2v*>(y);
+#define VSIG_R4_(UU)                                                                  \
+    if (ntl) hipLaunchKernelGGL((reduce4_probe<UU, true>), g, b, 0, st, x4, n4, y2);    \
+    else hipLaunchKernelGGL((reduce4_probe<UU, false>), g, b, 0, st, x4, n4, y2);
+    if (U == 2) { VSIG_R4_(2) } else if (U == 4) { VSIG_R4_(4) } else { VSIG_R4_(8) }
+#undef VSIG_R4_
+    return hipGetLastError();
+  }
   if (variant >= 16) {      // unrolled 8-B probes: 16 + (U index)*4 + NTL*2 + NTS
     const int ui = (variant - 16) / 4, ntl = (variant >> 1) & 1, nts = variant & 1;
     const int U = ui == 0 ? 4 : ui == 1 ? 8 : 16;
