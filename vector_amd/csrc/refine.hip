@@ -72,7 +72,10 @@ struct RefineKeys {
   unsigned long long max2;     // bits of the stage-2 max |c|^2
   unsigned long long negidx;   // INT64_MAX - lowest output index attaining max2
   unsigned long long status;   // 1: more than cap items (record left unrefined)
+  unsigned long long done;     // stage-2 blocks finished (the last one finishes)
+  unsigned long long nsurv;    // stage-2 survivors (listed in items while <= cap)
 };
+static_assert(sizeof(RefineKeys) <= 64, "the items follow the keys at +64 B");
 
 __device__ __forceinline__ double band_threshold(const PeakPartial* rec, double eps) {
   const double t = rec->max2 * (1.0 - eps);     // finalized record: max |c|
@@ -107,6 +110,131 @@ __global__ __launch_bounds__(256) void refine_select_array(
   }
 }
 
+// Finalize + select in one launch (the fused correlator's partials): block k
+// reduces partial chunk k into tmp[k] (fixed order); the last block to finish
+// reduces tmp into the record (max |c|), resets the refine keys and selects
+// the candidates: chunks whose max is in the band, their wave partials in the
+// band, and -- with lane keys -- the thread columns of those waves in the
+// band (items p * 64 + l), else the waves (items p).  Replaces the memset,
+// partial_chunks, partial_finalize and refine_select_partials launches.
+struct FinalizeSelect {
+  const PeakPartial* parts; long long nparts, chunk;
+  PeakPartial* tmp;                 // gridDim.x first-level records
+  unsigned long long* done;         // zero between launches (reset here)
+  PeakPartial* rec;                 // finalized record (max |c|)
+  double eps; long long cap;
+  long long* items; RefineKeys* keys;
+  const unsigned* lkeys;            // optional lane keys (64 per wave partial)
+};
+
+// A record another block of this launch wrote (possibly on another XCD).
+__device__ __forceinline__ PeakPartial ld_agent(const PeakPartial* p) {
+  PeakPartial r;
+  r.max2 = __hip_atomic_load(&p->max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.idx = __hip_atomic_load(&p->idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.sum_abs = __hip_atomic_load(&p->sum_abs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  r.sum_abs2 = __hip_atomic_load(&p->sum_abs2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return r;
+}
+
+__global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) {
+  const int tid = threadIdx.x;
+  __shared__ int slast, ncl;
+  __shared__ int clist[kFinalizeTmp];
+  __shared__ double cmax[kFinalizeTmp];
+  __shared__ unsigned long long scount;
+  __shared__ double sthr;
+  {
+    const long long lo = (long long)blockIdx.x * f.chunk;
+    const long long hi = lo + f.chunk < f.nparts ? lo + f.chunk : f.nparts;
+    double m = -1.0, s1 = 0.0, s2 = 0.0;
+    long long mi = 0x7fffffffffffffffLL;
+    for (long long i = lo + tid; i < hi; i += 256) {
+      const PeakPartial p = f.parts[i];
+      betterd(m, mi, p.max2, p.idx);
+      s1 += p.sum_abs;
+      s2 += p.sum_abs2;
+    }
+    block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
+  }
+  if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
+    __threadfence();
+    slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
+    if (slast) __threadfence();
+  }
+  __syncthreads();
+  if (!slast) return;
+  const int g1 = (int)gridDim.x;
+  {
+    double m = -1.0, s1 = 0.0, s2 = 0.0;
+    long long mi = 0x7fffffffffffffffLL;
+    for (int k = tid; k < g1; k += 256) {
+      const PeakPartial p = ld_agent(f.tmp + k);
+      cmax[k] = p.max2;
+      betterd(m, mi, p.max2, p.idx);
+      s1 += p.sum_abs;
+      s2 += p.sum_abs2;
+    }
+    __shared__ PeakPartial r[1];
+    block_partial<256>(m, mi, s1, s2, r);
+    __syncthreads();
+    if (tid == 0) {
+      PeakPartial o = r[0];
+      o.max2 = sqrt(o.max2);
+      *f.rec = o;
+      const double t = o.max2 * (1.0 - f.eps);
+      sthr = t > 0.0 ? t * t : 0.0;                // partials hold fp32 |c|^2
+      *f.done = 0;
+      ncl = 0;
+      scount = 0;
+    }
+    __syncthreads();
+  }
+  const double t2 = sthr;
+  for (int k = tid; k < g1; k += 256)
+    if (cmax[k] >= t2) clist[atomicAdd(&ncl, 1)] = k;
+  __syncthreads();
+  // the in-band chunks' partials, a wave per 64; a wave takes each hit's 64
+  // lane keys with one coalesced load and appends the in-band columns
+  const int lane = tid & 63;
+  const int nc = ncl;
+  for (int c = 0; c < nc; ++c) {
+    const long long lo = (long long)clist[c] * f.chunk;
+    const long long hi = lo + f.chunk < f.nparts ? lo + f.chunk : f.nparts;
+    for (long long pb = lo + (tid - lane); pb < hi; pb += 256) {   // uniform per wave
+      const long long p = pb + lane;
+      unsigned long long hits = __ballot(p < hi && f.parts[p].max2 >= t2);
+      while (hits) {
+        const int src = __builtin_ctzll(hits);
+        hits &= hits - 1;
+        const long long hp = pb + src;
+        bool take;
+        long long item;
+        if (f.lkeys) {
+          take = (double)__uint_as_float(f.lkeys[hp * 64 + lane] & ~63u) >= t2;
+          item = hp * 64 + lane;
+        } else {
+          take = lane == src;
+          item = hp;
+        }
+        const unsigned long long km = __ballot(take);
+        unsigned long long j0 = 0;
+        if (lane == 0) j0 = atomicAdd(&scount, (unsigned long long)__popcll(km));
+        j0 = __shfl(j0, 0);
+        const unsigned long long j = j0 + __popcll(km & ((1ull << lane) - 1));
+        if (take && (long long)j < f.cap) f.items[j] = item;
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    RefineKeys z{};
+    z.count = scount;
+    z.status = (long long)scount > f.cap ? 1ull : 0ull;
+    *f.keys = z;
+  }
+}
+
 struct RefineGeom {
   long long nout;       // outputs (final space)
   long long F;          // final output o is full-correlation index F + o
@@ -116,6 +244,8 @@ struct RefineGeom {
   long long hop;        // partial items: outputs per block, waves per block,
   int waves, Q, stride; //   rows per item and their stride,
   int wstep, rsub;      //   wave base step, 64-output rows per stride step
+  int cols;             // > 0: items are thread columns (wave p, column l) =
+                        //   p * 64 + l, cols rows each (xcorr_lane_keys)
 };
 
 __device__ __forceinline__ long long item_output(const RefineGeom& g, long long item, int q, int l) {
@@ -135,13 +265,21 @@ __device__ __forceinline__ long long item_output(const RefineGeom& g, long long 
   return g.rev ? g.nout - 1 - raw : raw;
 }
 
-// Stage 1: four blocks per (item, q) unit of 64 outputs, 16 outputs each:
-// thread (w, l) of a 16-wave block sums output 16 sub + (l & 15) over tap
-// chunk 4 w + (l >> 4) of 64 (independent partial sums, loads unrolled
-// 8-deep), the 64 chunk sums combined in LDS in chunk order.  (One block of
-// 64 outputs x 16 chunks ran a 32-batch dependent load chain per lane on 64
-// CUs; this is 8 batches on 256.)  vals / idx / cv are indexed by u * 64 + o,
-// u = item slot * Q + q, o the output's place in the unit.
+// Output po (< 64) of unit qu of an item: a wave item's unit qu is its row q
+// (64 outputs l); a column item has one unit, its rows q = po.
+__device__ __forceinline__ long long unit_output(const RefineGeom& g, long long item, int qu, int po) {
+  if (g.cols) return po < g.cols ? item_output(g, item >> 6, po, (int)(item & 63)) : -1;
+  return item_output(g, item, qu, po);
+}
+
+// Stage 1: 64 / OUTS blocks per unit of 64 outputs (a wave item's row q, or
+// a column item), OUTS outputs each: thread (w, l) of a 16-wave block sums
+// output OUTS sub + (l mod OUTS) over tap chunk (64 / OUTS) w + l / OUTS of
+// kS1Waves 64 / OUTS (independent partial sums, loads unrolled 8-deep), the
+// chunk sums combined in LDS in chunk order.  OUTS = 16 for wave items (64
+// chunks: 8 load batches for 4096 taps), 4 for the 64x fewer column items
+// (256 chunks, 2 batches).  vals / idx / cv are indexed by u * 64 + o, u =
+// item slot * Q + q, o the output's place in the unit.
 template <class T>
 __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __restrict__ v,
                                            long long abase, long long k0, long long k1,
@@ -170,37 +308,36 @@ __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __r
 }
 
 constexpr int kS1Waves = 16;
-constexpr int kS1Outs = 16;                         // outputs per block
-constexpr int kS1Chunks = kS1Waves * 64 / kS1Outs;  // tap chunks per output (64)
-constexpr int kS1Split = 64 / kS1Outs;              // blocks per unit (4)
 
-template <class T>
+template <class T, int OUTS>
 __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restrict__ a, const T* __restrict__ v,
                                                      RefineGeom g, const long long* __restrict__ items,
                                                      long long cap, RefineKeys* __restrict__ keys,
                                                      double* __restrict__ vals,
                                                      long long* __restrict__ oidx,
                                                      double2* __restrict__ cv) {
+  constexpr int kChunks = kS1Waves * 64 / OUTS;     // tap chunks per output
+  constexpr int kSplit = 64 / OUTS;                 // blocks per unit
   const long long cnt = (long long)keys->count;
   if (keys->status || cnt == 0) return;
   const long long nunits = (cnt < cap ? cnt : cap) * g.Q;
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ol = l & (kS1Outs - 1);                 // output within the block
-  const int ch = w * (64 / kS1Outs) + (l / kS1Outs); // tap chunk
-  __shared__ double pr[kS1Chunks][kS1Outs], pi[kS1Chunks][kS1Outs];
-  for (long long ub = blockIdx.x; ub < nunits * kS1Split; ub += gridDim.x) {   // uniform per block
-    const long long u = ub / kS1Split;
-    const int sub = (int)(ub - u * kS1Split);
+  const int ol = l & (OUTS - 1);                    // output within the block
+  const int ch = w * (64 / OUTS) + (l / OUTS);      // tap chunk
+  __shared__ double pr[kChunks][OUTS], pi[kChunks][OUTS];
+  for (long long ub = blockIdx.x; ub < nunits * kSplit; ub += gridDim.x) {   // uniform per block
+    const long long u = ub / kSplit;
+    const int sub = (int)(ub - u * kSplit);
     const long long item = items[u / g.Q];
     const int q = (int)(u % g.Q);
-    const int po = sub * kS1Outs + ol;              // output's place in the unit (0..63)
-    const long long o = item_output(g, item, q, po);
+    const int po = sub * OUTS + ol;                 // output's place in the unit (0..63)
+    const long long o = unit_output(g, item, q, po);
     double re = 0.0, im = 0.0;
     if (o >= 0) {
       const long long i = g.F + o;
       long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
-      const long long span = (k1 - k0 + kS1Chunks - 1) / kS1Chunks;   // this chunk's share
+      const long long span = (k1 - k0 + kChunks - 1) / kChunks;      // this chunk's share
       const long long q0 = k0 + ch * span;
       const long long q1 = q0 + span < k1 ? q0 + span : k1;
       if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im);
@@ -208,11 +345,11 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
     pr[ch][ol] = re;
     pi[ch][ol] = im;
     __syncthreads();
-    if (threadIdx.x < kS1Outs) {                    // lanes 0..15 of wave 0: output ol
+    if (threadIdx.x < OUTS) {                       // lanes 0..OUTS-1 of wave 0: output ol
       re = 0.0;
       im = 0.0;
 #pragma unroll 8
-      for (int c = 0; c < kS1Chunks; ++c) { re += pr[c][ol]; im += pi[c][ol]; }
+      for (int c = 0; c < kChunks; ++c) { re += pr[c][ol]; im += pi[c][ol]; }
       const double m2 = o >= 0 ? re * re + im * im : -1.0;
       const long long e = u * 64 + po;
       vals[e] = m2;
@@ -220,7 +357,7 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
       cv[e] = make_double2(re, im);
       double wm = m2;
 #pragma unroll
-      for (int off = kS1Outs / 2; off > 0; off >>= 1) {
+      for (int off = OUTS / 2; off > 0; off >>= 1) {
         const double o2 = __shfl_xor(wm, off);
         wm = o2 > wm ? o2 : wm;
       }
@@ -231,9 +368,13 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
 }
 
 // Stage 2: the outputs within eps2 of the stage-1 max recomputed by a
-// compensated dot product, one wave per output (lane l takes taps k = l mod
-// 64: Dot2 partials (s, c) per lane, combined across lanes by TwoSum, which
-// keeps Dot2's bound); the others drop out (vals = -1).
+// compensated dot product, one 1024-thread block per output (thread i takes
+// taps k = i mod 1024, four loads in flight: one batch for a 4096-tap
+// template; Dot2 partials (s, c) per thread, combined across lanes and then
+// across the 16 waves in wave order by TwoSum, which keeps Dot2's bound); the
+// others drop out (vals = -1).  The last block to finish takes the argmin
+// (the lowest output index attaining the max |c|^2, np.argmax's rule) and
+// writes the record (one launch instead of stage 2 + argmin + finish).
 __device__ __forceinline__ void two_sum_pair(double& s, double& c, double s2, double c2) {
   double t, e;
   two_sum(s, s2, t, e);
@@ -241,43 +382,62 @@ __device__ __forceinline__ void two_sum_pair(double& s, double& c, double s2, do
   c = c + c2 + e;
 }
 
+constexpr int kS2Threads = 1024;
+
 template <class T>
-__global__ __launch_bounds__(256) void refine_stage2(const T* __restrict__ a, const T* __restrict__ v,
-                                                     RefineGeom g, long long cap, double eps2,
-                                                     RefineKeys* __restrict__ keys,
-                                                     double* __restrict__ vals,
-                                                     const long long* __restrict__ oidx,
-                                                     double2* __restrict__ cv) {
+__global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict__ a, const T* __restrict__ v,
+                                                            RefineGeom g, long long cap, double eps2,
+                                                            RefineKeys* __restrict__ keys,
+                                                            double* __restrict__ vals,
+                                                            const long long* __restrict__ oidx,
+                                                            double2* __restrict__ cv,
+                                                            PeakPartial* __restrict__ rec,
+                                                            long long* __restrict__ items) {
+  constexpr int NW = kS2Threads / 64;
   const long long cnt = (long long)keys->count;
-  if (keys->status || cnt == 0) return;
+  if (keys->status || cnt == 0) return;            // uniform: no block counts itself
   const long long n = (cnt < cap ? cnt : cap) * g.Q * 64;
   const double m1 = __longlong_as_double((long long)keys->max1);
   const double thr = m1 * (1.0 - eps2);
-  const int l = threadIdx.x & 63;
-  const long long wave0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nwaves = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long base = wave0 * 64; base < n; base += nwaves * 64) {   // 64 entries per wave
-    const long long e = base + l;
-    const double v1 = e < n ? vals[e] : -1.0;
-    const bool surv = v1 >= 0.0 && v1 >= thr;
-    if (e < n && v1 >= 0.0 && !surv) vals[e] = -1.0;
-    unsigned long long mask = __ballot(surv);
-    while (mask) {
+  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  __shared__ unsigned long long smask;
+  __shared__ double ps[NW][4];
+  __shared__ int slast;
+  __shared__ long long smin;
+  for (long long base = (long long)blockIdx.x * 64; base < n; base += (long long)gridDim.x * 64) {
+    if (w == 0) {                                  // 64 entries per block step
+      const long long e = base + l;
+      const double v1 = e < n ? vals[e] : -1.0;
+      const bool surv = v1 >= 0.0 && v1 >= thr;
+      if (e < n && v1 >= 0.0 && !surv) vals[e] = -1.0;
+      const unsigned long long m = __ballot(surv);
+      if (l == 0) smask = m;
+      // the survivor list for the finish (items are free after stage 1)
+      unsigned long long j0 = 0;
+      if (l == 0 && m) j0 = atomicAdd(&keys->nsurv, (unsigned long long)__popcll(m));
+      j0 = __shfl(j0, 0);
+      const unsigned long long j = j0 + __popcll(m & ((1ull << l) - 1));
+      if (surv && (long long)j < cap) items[j] = e;
+    }
+    __syncthreads();
+    unsigned long long mask = smask;
+    while (mask) {                                 // uniform
       const int src = __builtin_ctzll(mask);
       mask &= mask - 1;
       const long long es = base + src;
-      const long long i = g.F + oidx[es];                 // uniform
+      const long long i = g.F + oidx[es];
       long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
       const long long abase = i - (g.nv - 1);
       double sr = 0.0, cr = 0.0, si = 0.0, ci = 0.0;
-      long long k = k0 + l;
-      // four taps' loads in flight per lane (the accumulation order is the
-      // one-tap loop's: same Dot2 result)
-      for (; k + 3 * 64 < k1; k += 4 * 64) {
+      long long k = k0 + tid;
+      for (; k + 3 * kS2Threads < k1; k += 4 * kS2Threads) {
         double2 x[4], y[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) { x[j] = ld2<T>(a, abase + k + 64 * j); y[j] = ld2<T>(v, k + 64 * j); }
+        for (int j = 0; j < 4; ++j) {
+          x[j] = ld2<T>(a, abase + k + kS2Threads * j);
+          y[j] = ld2<T>(v, k + kS2Threads * j);
+        }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           dot2_add(sr, cr, x[j].x, y[j].x);
@@ -286,7 +446,7 @@ __global__ __launch_bounds__(256) void refine_stage2(const T* __restrict__ a, co
           dot2_add(si, ci, -x[j].x, y[j].y);
         }
       }
-      for (; k < k1; k += 64) {
+      for (; k < k1; k += kS2Threads) {
         const double2 x = ld2<T>(a, abase + k);
         const double2 y = ld2<T>(v, k);
         dot2_add(sr, cr, x.x, y.x);
@@ -299,35 +459,60 @@ __global__ __launch_bounds__(256) void refine_stage2(const T* __restrict__ a, co
         two_sum_pair(sr, cr, __shfl_xor(sr, off), __shfl_xor(cr, off));
         two_sum_pair(si, ci, __shfl_xor(si, off), __shfl_xor(ci, off));
       }
-      if (l == 0) {
+      if (l == 0) { ps[w][0] = sr; ps[w][1] = cr; ps[w][2] = si; ps[w][3] = ci; }
+      __syncthreads();
+      if (tid == 0) {
+        sr = ps[0][0]; cr = ps[0][1]; si = ps[0][2]; ci = ps[0][3];
+        for (int q = 1; q < NW; ++q) {
+          two_sum_pair(sr, cr, ps[q][0], ps[q][1]);
+          two_sum_pair(si, ci, ps[q][2], ps[q][3]);
+        }
         const double re = sr + cr, im = si + ci;
         const double m2 = re * re + im * im;
         vals[es] = m2;
         cv[es] = make_double2(re, im);
         atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(m2));
       }
+      __syncthreads();
     }
   }
-}
-
-__global__ __launch_bounds__(256) void refine_argmin(long long cap, int Q,
-                                                     RefineKeys* __restrict__ keys,
-                                                     const double* __restrict__ vals,
-                                                     const long long* __restrict__ oidx) {
-  const long long cnt = (long long)keys->count;
-  if (keys->status || cnt == 0) return;
-  const long long n = (cnt < cap ? cnt : cap) * Q * 64;
-  const double m2 = __longlong_as_double((long long)keys->max2);
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride)
-    if (vals[e] == m2 && vals[e] >= 0.0)
-      atomicMax(&keys->negidx, (unsigned long long)(0x7fffffffffffffffLL - oidx[e]));
-}
-
-__global__ void refine_finish(RefineKeys* __restrict__ keys, PeakPartial* __restrict__ rec) {
-  if (keys->status || keys->count == 0 || keys->negidx == 0) return;
-  rec->max2 = sqrt(__longlong_as_double((long long)keys->max2));
-  rec->idx = 0x7fffffffffffffffLL - (long long)keys->negidx;
+  // the last block to finish: argmin over the entries, then the record (one
+  // release per block: the block's stores are complete at the barrier above)
+  __syncthreads();
+  if (tid == 0) {
+    __threadfence();
+    slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)gridDim.x - 1;
+    if (slast) __threadfence();
+    smin = 0x7fffffffffffffffLL;
+  }
+  __syncthreads();
+  if (!slast) return;
+  const double m2 = __longlong_as_double(
+      (long long)__hip_atomic_load(&keys->max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  long long mi = 0x7fffffffffffffffLL;
+  const long long ns = (long long)__hip_atomic_load(&keys->nsurv, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+  const bool listed = ns <= cap;                   // else every entry
+  const long long ne = listed ? ns : n;
+  for (long long q = tid; q < ne; q += kS2Threads) {
+    const long long e = listed ? __hip_atomic_load(&items[q], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_AGENT) : q;
+    const double ve = __hip_atomic_load(&vals[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (ve == m2 && ve >= 0.0) {
+      const long long o = oidx[e];
+      mi = o < mi ? o : mi;
+    }
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    const long long om = __shfl_xor(mi, off);
+    mi = om < mi ? om : mi;
+  }
+  if (l == 0) atomicMin(&smin, mi);
+  __syncthreads();
+  if (tid == 0 && smin != 0x7fffffffffffffffLL) {
+    rec->max2 = sqrt(m2);
+    rec->idx = smin;
+  }
 }
 
 // Refined values into a complex128 output (stage-2 values where computed,
@@ -353,7 +538,7 @@ size_t refine_scratch_bytes(long long cap_items, int Q) {
 }
 
 hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
-  if (r.cap_items < 1) return hipErrorInvalidValue;
+  if (r.cap_items < 1 || (r.cols && (r.from_array || r.cols > 64))) return hipErrorInvalidValue;
   char* base = static_cast<char*>(r.scratch);
   RefineKeys* keys = reinterpret_cast<RefineKeys*>(base);
   const long long n = r.cap_items * r.Q * 64;
@@ -361,45 +546,60 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   double* vals = reinterpret_cast<double*>(items + r.cap_items);
   long long* oidx = reinterpret_cast<long long*>(vals + n);
   double2* cv = reinterpret_cast<double2*>(oidx + n);
-  hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
-  if (e != hipSuccess) return e;
   RefineGeom g{r.nout, r.F, r.na, r.nv, r.rev, r.from_array, r.hop, r.waves, r.Q, r.stride,
-               r.wstep, r.rsub};
+               r.wstep, r.rsub, r.cols};
   PeakPartial* rec = r.rec;
-  if (r.from_array) {
-    const long long grid = (r.nout + 255) / 256;
-    hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
-                       rec, r.eps, r.cap_items, items, keys);
+  if (r.finalize) {              // the partials' finalize + select in one launch
+    if (r.from_array || !r.tmp || !r.done) return hipErrorInvalidValue;
+    long long g1 = (r.nparts + 2047) / 2048;
+    if (g1 < 1) g1 = 1;
+    if (g1 > kFinalizeTmp) g1 = kFinalizeTmp;
+    long long chunk = (r.nparts + g1 - 1) / g1;
+    if (chunk < 1) chunk = 1;
+    g1 = (r.nparts + chunk - 1) / chunk;
+    if (g1 < 1) g1 = 1;
+    const FinalizeSelect f{r.parts, r.nparts, chunk, r.tmp, r.done, rec, r.eps, r.cap_items,
+                           items, keys, r.lkeys};
+    hipLaunchKernelGGL(refine_finalize_select, dim3((unsigned)g1), dim3(256), 0, st, f);
   } else {
-    const long long grid = (r.nparts + 255) / 256;
-    hipLaunchKernelGGL(refine_select_partials, dim3((unsigned)grid), dim3(256), 0, st, r.parts,
-                       r.nparts, rec, r.eps, r.cap_items, items, keys);
+    if (r.cols || r.lkeys) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
+    if (e != hipSuccess) return e;
+    if (r.from_array) {
+      const long long grid = (r.nout + 255) / 256;
+      hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
+                         rec, r.eps, r.cap_items, items, keys);
+    } else {
+      const long long grid = (r.nparts + 255) / 256;
+      hipLaunchKernelGGL(refine_select_partials, dim3((unsigned)grid), dim3(256), 0, st, r.parts,
+                         r.nparts, rec, r.eps, r.cap_items, items, keys);
+    }
   }
-  // stage grids: stage 1 kS1Split blocks per unit (grid-stride), stage 2 one
-  // wave per 64 entries (grid-stride), capped at a few blocks per CU
-  long long units = r.cap_items * r.Q * kS1Split;
-  if (units > 8192) units = 8192;
+  // stage grids (grid-stride over the device-side candidate count): stage 1
+  // 64 / OUTS blocks per unit, stage 2 one block per 64 entries, capped so
+  // that the usual few candidates do not pay for thousands of idle blocks
+  const int split = r.cols ? 16 : 4;
+  long long units = r.cap_items * r.Q * split;
+  if (units > 1024) units = 1024;
   const unsigned g1 = (unsigned)units;
-  long long g2l = (n + 255) / 256;
-  if (g2l > 4096) g2l = 4096;
+  long long g2l = n / 64;
+  if (g2l > 256) g2l = 256;
   const unsigned g2 = (unsigned)g2l;
-  if (r.c128) {
-    const double2* a = static_cast<const double2*>(r.a);
-    const double2* v = static_cast<const double2*>(r.v);
-    hipLaunchKernelGGL(refine_stage1<double2>, dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
-                       r.cap_items, keys, vals, oidx, cv);
-    hipLaunchKernelGGL(refine_stage2<double2>, dim3(g2), dim3(256), 0, st, a, v, g, r.cap_items,
-                       r.eps2, keys, vals, oidx, cv);
-  } else {
-    const float2* a = static_cast<const float2*>(r.a);
-    const float2* v = static_cast<const float2*>(r.v);
-    hipLaunchKernelGGL(refine_stage1<float2>, dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
-                       r.cap_items, keys, vals, oidx, cv);
-    hipLaunchKernelGGL(refine_stage2<float2>, dim3(g2), dim3(256), 0, st, a, v, g, r.cap_items,
-                       r.eps2, keys, vals, oidx, cv);
-  }
-  hipLaunchKernelGGL(refine_argmin, dim3(g2), dim3(256), 0, st, r.cap_items, r.Q, keys, vals, oidx);
-  hipLaunchKernelGGL(refine_finish, dim3(1), dim3(1), 0, st, keys, rec);
+  auto stages = [&](auto tag) {
+    using T = decltype(tag);
+    const T* a = static_cast<const T*>(r.a);
+    const T* v = static_cast<const T*>(r.v);
+    if (r.cols)
+      hipLaunchKernelGGL((refine_stage1<T, 4>), dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
+                         r.cap_items, keys, vals, oidx, cv);
+    else
+      hipLaunchKernelGGL((refine_stage1<T, 16>), dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
+                         r.cap_items, keys, vals, oidx, cv);
+    hipLaunchKernelGGL(refine_stage2<T>, dim3(g2), dim3(kS2Threads), 0, st, a, v, g, r.cap_items,
+                       r.eps2, keys, vals, oidx, cv, rec, items);
+  };
+  if (r.c128) stages(double2{});
+  else stages(float2{});
   if (r.out128)
     hipLaunchKernelGGL(refine_patch, dim3(g2), dim3(256), 0, st, r.cap_items, r.Q, keys, oidx, cv,
                        static_cast<double2*>(r.out128));

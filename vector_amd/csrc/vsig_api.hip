@@ -31,6 +31,8 @@ struct vsig_ctx {
   size_t conv_bytes[3] = {0, 0, 0};
   void* rscratch = nullptr;              // refine.hip scratch (keys first)
   size_t rscratch_bytes = 0;
+  void* lkeys = nullptr;                 // correlator lane keys (refine column candidates)
+  size_t lkeys_bytes = 0;
   int refine = 1;                        // exact re-rank of the correlators' peak
   int refine_eps_ppm = 1000;             // fp32 candidate band (relative, ppm of max |c|)
   long long refine_cap = 1LL << 20;      // max outputs revisited (else record left fp32)
@@ -162,8 +164,10 @@ int ensure_partials(vsig_ctx* c, long long n) {
   c->partials = nullptr;
   c->npartials = 0;
   long long cap = n < 4096 ? 4096 : n + n / 4;
-  // + the first-level buffer of a two-level finalize, right after the partials
-  HIPCHK(c, hipMalloc(&c->partials, (cap + vsig::kFinalizeTmp) * sizeof(PeakPartial)));
+  // + the first-level buffer of a two-level finalize, right after the partials,
+  // and the fused finalize's block counter (zero between launches)
+  HIPCHK(c, hipMalloc(&c->partials, (cap + vsig::kFinalizeTmp + 1) * sizeof(PeakPartial)));
+  HIPCHK(c, hipMemset(c->partials + cap + vsig::kFinalizeTmp, 0, sizeof(PeakPartial)));
   c->npartials = cap;
   return VSIG_OK;
 }
@@ -268,10 +272,14 @@ struct RefineOperands {
 // Re-rank the peak record rec (finalized, max |c|) over the outputs within the
 // fp32 band; src: the correlator's wave partials (geometry of an M-point
 // launch with raw->final reversal rev) or, if c64 != null, a stored c64 array.
+// fused: the correlator's partials are not finalized yet -- the refine's first
+// launch finalizes them into rec and selects (thread columns when lkeys).
 int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, long long hop,
-               long long nparts, int rev, const float2* c64, PeakPartial* rec, void* out128) {
+               long long nparts, int rev, const float2* c64, PeakPartial* rec, void* out128,
+               bool fused = false, const unsigned* lkeys = nullptr) {
   c->refine_ran = false;
-  if (!c->refine) return VSIG_OK;
+  if (!c->refine) return fused ? fail(c, VSIG_E_INVALID, "refine: fused finalize with refine off")
+                             : VSIG_OK;
   vsig::RefineArgs r{};
   r.a = op.a; r.na = op.na; r.v = op.v; r.nv = op.nv; r.c128 = op.c128;
   r.nout = nout; r.F = op.F; r.rev = rev;
@@ -284,6 +292,14 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
       return fail(c, VSIG_E_INVALID, "refine: no correlator geometry for M");
     r.parts = c->partials; r.nparts = nparts; r.hop = hop;
     r.waves = waves; r.Q = Q; r.stride = stride; r.wstep = wstep; r.rsub = rsub;
+    if (fused) {
+      r.finalize = 1;
+      r.tmp = c->partials + c->npartials;
+      r.done = reinterpret_cast<unsigned long long*>(r.tmp + vsig::kFinalizeTmp);
+    }
+    if (lkeys) {                 // items = thread columns of Q rows, one unit each
+      r.cols = Q; r.lkeys = lkeys; r.Q = 1;
+    }
   }
   r.eps = c->refine_eps_ppm * 1e-6;
   r.eps2 = 1e-6;
@@ -498,6 +514,7 @@ void vsig_free(vsig_ctx* c) {
   for (int i = 0; i < 3; ++i) if (c->stage[i]) (void)hipFree(c->stage[i]);
   for (int i = 0; i < 3; ++i) if (c->conv[i]) (void)hipFree(c->conv[i]);
   if (c->rscratch) (void)hipFree(c->rscratch);
+  if (c->lkeys) (void)hipFree(c->lkeys);
   for (auto& kv : c->chirps) { (void)hipFree(kv.second.c); (void)hipFree(kv.second.B); }
   if (c->bigtmp) (void)hipFree(c->bigtmp);
   for (int i = 0; i < 2; ++i) if (c->spec[i]) (void)hipFree(c->spec[i]);
@@ -858,6 +875,16 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     const long long nparts = nblocks * waves;   // one partial per wave
     int rc = ensure_partials(c, nparts);
     if (rc) return rc;
+    // with the refine on, the partials' finalize and the candidate select run
+    // as the refine's first launch, on thread columns where the kernel writes
+    // lane keys (64x fewer outputs re-ranked than whole waves)
+    const bool fused = op && c->refine && !(store_mode & 8);
+    unsigned* lk = nullptr;
+    if (fused && Q <= 64 && vsig::xcorr_lane_keys(x->M) == Q) {
+      if ((rc = ensure_buf(c, &c->lkeys, &c->lkeys_bytes, (size_t)nparts * 64 * sizeof(unsigned))))
+        return rc;
+      lk = static_cast<unsigned*>(c->lkeys);
+    }
     const float2* tw;
     const float2* wt = nullptr;
     if ((rc = get_twiddles(c, plan, &tw))) return rc;
@@ -865,12 +892,15 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     {
       Timed t(c, "xcorr");
       HIPCHK(c, vsig::launch_xcorr_os(x->M, s, n, x->Ps[0], off, nout, hop, cout, store_mode,
-                                      c->partials, tw, wt, c->stream));
+                                      c->partials, tw, wt, c->stream, lk));
     }
-    if ((rc = finalize_peak(c, nparts, 1, peak_dev))) return rc;
-    if (!op) return VSIG_OK;
+    if (!fused) {
+      if ((rc = finalize_peak(c, nparts, 1, peak_dev))) return rc;
+      if (!op) return VSIG_OK;
+    }
     if (out128 && cout) HIPCHK(c, vsig::launch_convert_c(1, cout, nout, out128, c->stream));
-    return run_refine(c, *op, nout, x->M, hop, nparts, (store_mode & 4) ? 1 : 0, nullptr, rec, out128);
+    return run_refine(c, *op, nout, x->M, hop, nparts, (store_mode & 4) ? 1 : 0, nullptr, rec, out128,
+                      fused, lk);
   }
   constexpr long long B = 8192;
   constexpr int M = 16384;

@@ -121,7 +121,11 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, const float2* wt,
-                           hipStream_t st);
+                           hipStream_t st, unsigned* lkeys = nullptr);
+// Rows per thread column if the correlator for M can write lane keys
+// (lkeys[b TF + m(t)]: thread t's max |c|^2 key, the refine's column
+// candidates), else 0.
+int xcorr_lane_keys(int M);
 // Outputs of wave w of block b of the correlator for M (the refine pass's
 // items): ob + wstep w + l + 64 (q % rsub) + stride (q / rsub), l < 64, q < Q.
 hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* wstep, int* rsub);
@@ -152,6 +156,11 @@ struct RefineArgs {
   int waves, Q, stride;             // wave w of block b: ob + wstep w + l + 64 (q % rsub)
   int wstep, rsub;                  //   + stride (q / rsub), l < 64, q < Q (xcorr_geom)
   double eps, eps2;                 // fp32 band, stage-2 band (relative)
+  int cols;                         // > 0: thread-column items from lane keys (Q = 1;
+  const unsigned* lkeys;            //   cols rows each), lkeys: 64 per wave partial
+  int finalize;                     // finalize the partials here (+ select, one launch):
+  PeakPartial* tmp;                 //   kFinalizeTmp first-level records,
+  unsigned long long* done;         //   a counter that is zero between launches
   long long cap_items;
   void* scratch;                    // refine_scratch_bytes(cap_items, Q)
   PeakPartial* rec;                 // finalized record (max |c|), updated in place

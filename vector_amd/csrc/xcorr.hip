@@ -227,7 +227,7 @@ template <class P>
 __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float2* d, long long b,
                                                     long long hop, long long nout,
                                                     float2* __restrict__ c, int store_mode,
-                                                    PeakPartial* partials, int t) {
+                                                    PeakPartial* partials, unsigned* lkeys, int t) {
   constexpr int H = P::N;
   const long long ob = b * hop;
   const long long rem = nout - ob;
@@ -296,6 +296,8 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
       constexpr int e = decltype(ei)::value;
       acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
     });
+    // lane keys (refine candidates per thread column, see xcorr_lane_keys)
+    if (lkeys) lkeys[b * P::TF + tmapl<P>(t)] = key;
     const int rank = (int)((key & 63u) ^ rx);
     const int mi = tmapl<P>(t) + KR::kStep * rank;
     const float m = any ? __uint_as_float(key & ~63u) : -1.f;
@@ -339,7 +341,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw,
-    const float2* __restrict__ wt, bool x4) {
+    const float2* __restrict__ wt, bool x4, unsigned* __restrict__ lkeys) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   constexpr int M = 2 * P::N;
   static_assert(P::TF % (M / 64) == 0 && (P::N / P::R[0]) % (M / 64) == 0,
@@ -380,27 +382,28 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
   });
-  xcorr_half_epilogue<P>(a, d, b, hop, nout, c, store_mode, partials, t);
+  xcorr_half_epilogue<P>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
 }
 
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
                            long long nout, long long hop, float2* c, int store_mode,
                            PeakPartial* partials, const float2* tw, const float2* wt,
-                           hipStream_t st) {
+                           hipStream_t st, unsigned* lkeys) {
   if (nout <= 0) return hipSuccess;
+  if (lkeys && !xcorr_lane_keys(M)) return hipErrorInvalidValue;
   const long long nblocks = (nout + hop - 1) / hop;
   if (M == 16384) {
     // every segment start s - off + b hop 16-byte aligned: 16-byte loads
     const bool x4 = hop % 2 == 0 && ((reinterpret_cast<uintptr_t>(s) - 8 * (uintptr_t)off) & 15) == 0;
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt, x4);
+                       partials, nblocks, tw, wt, x4, lkeys);
     return hipGetLastError();
   }
   if (M == 32768) {     // 16384-point halves, one block per CU
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX32k>, dim3((unsigned)nblocks), dim3(PlanX32k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt, false);
+                       partials, nblocks, tw, wt, false, lkeys);
     return hipGetLastError();
   }
   auto run = [&](auto plan) {
@@ -414,6 +417,22 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   else if (M == 8192) run(Plan8192{});
   else return hipErrorInvalidValue;
   return hipGetLastError();
+}
+
+// Rows per thread column when the correlator for M writes lane keys (the
+// keyed epilogue: thread t of block b stores its max key at b TF + m(t),
+// m(t) = its last-pass butterfly base, which is column m(t) mod 64 of wave
+// m(t) / 64 in xcorr_geom's terms), else 0.
+// The column's outputs m(t) + kStep R (R < 2E) are xcorr_geom's rows q = R
+// when kStep is the row stride TF.
+template <class P>
+constexpr int lane_key_rows() {
+  return KeyedRank<P>::ok && KeyedRank<P>::kStep == P::TF && 2 * P::E <= 64 ? 2 * P::E : 0;
+}
+int xcorr_lane_keys(int M) {
+  if (M == 16384) return lane_key_rows<PlanX16k>();
+  if (M == 32768) return lane_key_rows<PlanX32k>();
+  return 0;
 }
 
 // Wave geometry of the correlator's partials (see the header comment):
