@@ -178,6 +178,8 @@ class StreamChain:
         self.y_ext = backend.empty(self.ny + max(self.L - 1, 0))     # [chunk out | right halo]
         self.sxx = backend.empty((self.ny // cfg.nfft) * cfg.nfft, torch.float32)
         self.recs = backend.empty(4 * cfg.pipeline, torch.float64).view(cfg.pipeline, 4)
+        # every rank's records, gathered in place (one collective, no copies)
+        self.rows = backend.empty(4 * cfg.pipeline * world, torch.float64).view(world * cfg.pipeline, 4)
         self.peak_rows = None
 
     @property
@@ -188,6 +190,10 @@ class StreamChain:
     @property
     def y(self):
         return self.y_ext[: self.ny]
+
+    def _gather_peaks(self):
+        dist.all_gather_into_tensor(self.rows, self.recs, group=self.group)
+        return list(self.rows.view(self.world, self.cfg.pipeline, 4).unbind(0))
 
     def _exchange_start(self, send, dst, recv, src):
         ops = []
@@ -277,9 +283,7 @@ class StreamChain:
             be.join()
         if L:
             if w > 1:                           # 6. global peak records
-                rows = [torch.empty_like(self.recs) for _ in range(w)]
-                dist.all_gather(rows, self.recs, group=self.group)
-                self.peak_rows = rows
+                self.peak_rows = self._gather_peaks()
             else:
                 self.peak_rows = [self.recs]
 
@@ -303,9 +307,7 @@ class StreamChain:
             halo = (L - 1) if r < w - 1 else 0
             be.xcorr_peak(self.y_ext[: ny + halo], self.recs[0])
             if w > 1:
-                rows = [torch.empty_like(self.recs) for _ in range(w)]
-                dist.all_gather(rows, self.recs, group=self.group)
-                self.peak_rows = rows
+                self.peak_rows = self._gather_peaks()
             else:
                 self.peak_rows = [self.recs]
         else:
@@ -346,9 +348,7 @@ class StreamChain:
         consume(K - 1)
         if L:
             if w > 1:
-                rows = [torch.empty_like(self.recs) for _ in range(w)]
-                dist.all_gather(rows, self.recs, group=self.group)
-                self.peak_rows = rows
+                self.peak_rows = self._gather_peaks()
             else:
                 self.peak_rows = [self.recs]
 
