@@ -199,3 +199,29 @@ def test_input_dtypes(gpu, dt):
     c, lags = gpu.cross_correlate_signals(t, s, "full")
     assert c.dtype == np.complex128
     assert gpu.find_correlation_peak(c, lags)[0] == want[0]
+
+
+@pytest.mark.parametrize("L", [700, 2048, 4096, 8000, 12_000])
+@pytest.mark.parametrize("ratio", [1 + 1e-9, 1 - 1e-9])
+@pytest.mark.parametrize("swapped", [False, True])
+def test_near_tie_columns_every_plan(gpu, L, ratio, swapped):
+    """Two copies 1e-9 apart in amplitude whose peaks lie L + 197 outputs
+    apart (other thread columns, where the correlator writes lane keys: M =
+    16384 / 32768; whole waves at M = 4096 / 8192), in both operand orders
+    (swapped: the template is the first operand, the kernel's outputs
+    reversed): numpy's lag exactly, the peak to 1e-12."""
+    n = 3 * L + 40_000
+    pre = ref.qpsk_preamble(L, seed=L + 1)
+    s = np.zeros(n, np.complex128)
+    s[: n // 4] = 0.01 * ref.synth_iq(n // 4, seed=L)
+    k1 = n // 3
+    k2 = k1 + L + 197
+    s[k1:k1 + L] += pre
+    s[k2:k2 + L] += ratio * pre.astype(np.complex128)
+    a, b = (s, pre) if swapped else (pre, s)
+    mode = "full" if swapped else "valid"
+    want = ref.find_correlation_peak(*ref.cross_correlate_signals(a, b, mode))
+    lag, val, _ = gpu.correlate_peak(a, b, mode)
+    assert lag == want[0]
+    assert val == pytest.approx(want[1], rel=1e-12)
+    assert _status(gpu)[0] == 0
