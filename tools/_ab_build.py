@@ -16,6 +16,8 @@ VARIANTS = {
     "libvsig_pfb128": ("VSIG_PFB_FPG=128",),
     "libvsig_pfb256": ("VSIG_PFB_FPG=256",),
     "libvsig_pfb512": ("VSIG_PFB_FPG=512",),
+    "libvsig_ilv50": ("VSIG_ILV_S=5", "VSIG_ILV_U=0"),
+    "libvsig_ilv61": ("VSIG_ILV_S=6", "VSIG_ILV_U=1"),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

@@ -261,8 +261,18 @@ struct mapl_of { static constexpr int value = kMapId; };
 template <class P>
 struct mapl_of<P, decltype(void(P::MAPL))> { static constexpr int value = P::MAPL; };
 
+template <class P, class = void>
+struct padun_of { static constexpr int value = 0; };
 template <class P>
-__device__ __forceinline__ int lpadp(int i) { return i + (i >> padsh_of<P>::value); }
+struct padun_of<P, decltype(void(P::PADUN))> { static constexpr int value = P::PADUN; };
+// padding before index i: 2^PADUN float2 per 2^PADSH (PADUN = 1 keeps even
+// indices 16-byte aligned: adjacent pairs become one ds_read/write_b128)
+template <class P>
+__host__ __device__ constexpr int padc(int i) {
+  return (i >> padsh_of<P>::value) << padun_of<P>::value;
+}
+template <class P>
+__device__ __forceinline__ int lpadp(int i) { return i + padc<P>(i); }
 template <int MAP>
 __device__ __forceinline__ int lane_map(int t) {
   if constexpr (MAP == kMapSigma) return (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1);
@@ -291,16 +301,17 @@ __device__ __forceinline__ int bfly(int t, int b) {
 }
 
 // A plan with its exchange geometry set (see above).
-template <class P, int M0, int ML, int S = 5>
+template <class P, int M0, int ML, int S = 5, int U = 0>
 struct Lanes : P {
   static_assert(M0 != kMapPair || P::TF == 64, "the pair map is for one-wave frames");
   static_assert((M0 != kMapIlv || P::E / P::R[0] == 2) && (ML != kMapIlv || P::E / P::RL == 2),
                 "the interleaved map pairs two butterflies per thread");
   static_assert(P::TF % 64 == 0 && (P::N / P::R[0]) % 32 == 0, "maps permute 32-lane runs");
   static constexpr int PADSH = S;
+  static constexpr int PADUN = U;
   static constexpr int MAP0 = M0;
   static constexpr int MAPL = ML;
-  static constexpr int LDS = P::N + (P::N >> S);
+  static constexpr int LDS = P::N + ((P::N >> S) << U);
 };
 template <class P>
 using Swz = Lanes<P, kMapSigma, kMapSigma, 5>;
@@ -519,21 +530,22 @@ __device__ __forceinline__ void fft_stage(float2* v, TW tws, int t, H hook = H{}
   }
 }
 
-// lpad(base + c) for a compile-time c: multiples of 16 become an immediate
-// offset from lpad(base) (lpad(b + 16m) = lpad(b) + 17m), so a pass needs one
-// LDS base address per butterfly instead of one per element.
+// lpad(base + c) for a compile-time c: multiples of 2^S become an immediate
+// offset from lpad(base) (lpad(b + 16m) = lpad(b) + 17m at S = 4), so a pass
+// needs one LDS base address per butterfly instead of one per element.
 template <class P, int C>
 __device__ __forceinline__ int lpad_off(int base, int base_pad) {
   constexpr int S = padsh_of<P>::value;
-  if constexpr (C % (1 << S) == 0) return base_pad + C + (C >> S);
+  if constexpr (C % (1 << S) == 0) return base_pad + C + padc<P>(C);
   else return lpadp<P>(base + C);
 }
 
 // Padded LDS index of butterfly j's output 0 in pass p, such that output r
-// sits at store_base + C + (C >> S), C = r Ns (S = padsh): the destination
-// base + C, base = hi + lo with hi = (j / Ns) Ns R, lo = j mod Ns, pads as
-//   Ns >= 2^S : lpad(base) + C + (C >> S)             (C a multiple of 2^S);
-//   Ns <  2^S : base + (hi >> S) + C + (C >> S)       (lo + C never carries
+// sits at store_base + C + pad(C), C = r Ns (pad(i) = padc: (i >> S) << U):
+// the destination base + C, base = hi + lo with hi = (j / Ns) Ns R, lo = j
+// mod Ns, pads as
+//   Ns >= 2^S : lpad(base) + C + pad(C)               (C a multiple of 2^S);
+//   Ns <  2^S : base + pad(hi) + C + pad(C)           (lo + C never carries
 //               past bit S into hi's multiple of 2^S, or stays below Ns R <=
 //               2^S) -- one address per butterfly, immediate offsets per r.
 template <class P, int p>
@@ -544,7 +556,7 @@ __device__ __forceinline__ int store_base(int j) {
   const int hi = (j / Ns) * Ns * R;
   const int base = hi + (j & (Ns - 1));
   if constexpr (Ns >= (1 << S)) return lpadp<P>(base);
-  else return base + (hi >> S);
+  else return base + padc<P>(hi);
 }
 
 template <class P, int p>
@@ -559,7 +571,7 @@ __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
       constexpr int C = r * Ns;
-      lds[bp + C + (C >> padsh_of<P>::value)] = v[b * R + r];
+      lds[bp + C + padc<P>(C)] = v[b * R + r];
     });
   });
 }
@@ -569,13 +581,16 @@ __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
   if constexpr (pass_map<P, p>() == kMapIlv) {
+    // butterflies 2t, 2t + 1 share one padded base (never split by a pad:
+    // S >= 1); with U = 1 the base is even, so each r is one 16-byte read
+    static_assert(B == 2 && (P::N / R) % (1 << padsh_of<P>::value) == 0, "interleaved pairs");
+    const int jb = bfly<P, p>(t, 0);
+    const int jp = lpadp<P>(jb);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
-      const int jb = bfly<P, p>(t, b);
-      const int jp = lpadp<P>(jb);
       static_for<0, R>([&](auto ri) {
         constexpr int r = decltype(ri)::value;
-        v[b * R + r] = lds[lpad_off<P, r * (P::N / R)>(jb, jp)];
+        v[b * R + r] = lds[jp + b + r * (P::N / R) + padc<P>(r * (P::N / R))];
       });
     });
   } else {
@@ -606,7 +621,7 @@ __device__ __forceinline__ void fft_store_c(const float2* v, float* lds, int t) 
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
       constexpr int O = r * Ns;
-      lds[bp + O + (O >> padsh_of<P>::value)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
+      lds[bp + O + padc<P>(O)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
     });
   });
 }
@@ -803,7 +818,11 @@ using Plan1024x = Lanes<Plan1024s, kMapPair, kMapPair>;
 using Plan8192x = Swz<Plan8192>;
 // The PSD's 8192-point plan with interleaved first / last passes (16-byte
 // frame loads, 8-byte |X|^2 stores, conflict-free exchanges).
-using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, 5>;
+#ifndef VSIG_ILV_S            // tuning builds: the interleaved plan's padding
+#define VSIG_ILV_S 5
+#define VSIG_ILV_U 1
+#endif
+using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, VSIG_ILV_S, VSIG_ILV_U>;
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

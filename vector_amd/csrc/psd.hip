@@ -33,7 +33,7 @@ __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
     const float2* __restrict__ tw, bool x4) {
   static_assert(P::TF >= 256, "one frame per block");
-  __shared__ float2 lds[P::LDS];
+  __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
   const int t = threadIdx.x;
   const long long u = blockIdx.x;
   float2 wa[nanch_total<P>()];
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(P::TF) void fft_bench_kernel(float2* __restrict__ i
 template <class P, int PAIR>
 __global__ __launch_bounds__(P::TF, 2) void fft_bench_anch_kernel(float2* __restrict__ io, int iters,
                                                                   const float2* __restrict__ tw) {
-  __shared__ float2 lds[P::LDS];
+  __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
   const int t = threadIdx.x;
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
