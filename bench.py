@@ -168,7 +168,9 @@ def main():
     ap.add_argument("--decim", type=int, default=None, help="(default: the workload's)")
     ap.add_argument("--nfft", type=int, default=8192)
     ap.add_argument("--template", type=int, default=4096)
-    ap.add_argument("--cpu-samples", type=int, default=1 << 22)
+    ap.add_argument("--cpu-samples", type=int, default=None,
+                    help="CPU-baseline sample (default: ~10-15 s of single-core work: "
+                         "2**26 samples for the chains, 2**24 for sync, 2**27 for pfb)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=16,
                     help="processes for the all-cores CPU baseline (the GPU box's CPU share is 16)")
@@ -342,7 +344,7 @@ def main():
                            "bytes_basis": f"{chain_bytes / n:.2f} B/input sample"}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
-        cs = args.cpu_samples
+        cs = args.cpu_samples or (1 << 26)
         cpu = cpu_baseline(cs, taps, args.nfft, tmpl, decim)
         cpu["cores_available"] = len(os.sched_getaffinity(0))
         if args.cpu_workers > 1:
@@ -439,14 +441,14 @@ def run_sync(args, world, rank, local, dev):
     cpu = None
     if not args.no_cpu_baseline:
         from oracle import ref        # the CPU baseline leg only
-        ns = 1 << 21
+        ns = args.cpu_samples or (1 << 24)
         xs = ref.synth_iq(ns, seed=99)
         t1 = time.perf_counter()
         c, lags = ref.cross_correlate_signals(pre, xs, "valid")
         ref.find_correlation_peak(c, lags)
         dt = time.perf_counter() - t1
         cpu = dict(value=round(ns / dt / 1e6, 3), unit="Msamples/s", cores=1, kind="port",
-                   sample=(f"{ns} samples (2**21) through np.correlate complex128 L={L} valid + "
+                   sample=(f"{ns} samples (2**{int(np.log2(ns))}) through np.correlate complex128 L={L} valid + "
                            f"find_correlation_peak, {dt:.2f} s, 1 thread (direct O(N L); the "
                            f"full 2**30 stream would take ~{n / (ns / dt) / 60:.0f} min)"),
                    seconds=round(dt, 3), cores_available=len(os.sched_getaffinity(0)))
@@ -536,7 +538,7 @@ def run_pfb(args, world, rank, local, dev):
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         from oracle import ref        # the CPU baseline leg only
-        ns = 1 << 22
+        ns = args.cpu_samples or (1 << 27)
         xs = ref.synth_iq(ns, seed=99)
         t0 = time.perf_counter()
         ref.pfb_channelize(xs, proto, nchan)
