@@ -225,3 +225,28 @@ def test_near_tie_columns_every_plan(gpu, L, ratio, swapped):
     assert lag == want[0]
     assert val == pytest.approx(want[1], rel=1e-12)
     assert _status(gpu)[0] == 0
+
+
+def test_flat_correlation_over_cap_is_cheap(gpu):
+    """A tone against itself over 2^24 samples (M = 16384, 5461 blocks, three
+    finalize chunks): every thread column is in the band, far past the default
+    cap of 2^20 outputs; the fused finalize stops appending at the cap, the
+    record stays the fp32 one (status 1) and the pass costs milliseconds."""
+    import time
+    n, L = 1 << 24, 4096
+    ph = 2 * np.pi * 0.01 * np.arange(n)
+    tone = torch.polar(torch.ones(n, dtype=torch.float64),
+                       torch.from_numpy(ph)).to(torch.complex64).cuda()
+    tmpl = tone[:L].cpu().numpy()
+    with pytest.warns(RuntimeWarning, match="refine_cap"):
+        gpu.correlate_peak(tmpl, tone, "valid")      # warm-up (plans, scratch)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    with pytest.warns(RuntimeWarning, match="refine_cap"):
+        lag, val, _ = gpu.correlate_peak(tmpl, tone, "valid")
+    dt = time.perf_counter() - t0
+    st, cand = _status(gpu)
+    assert st == 1 and cand > (1 << 20) // 64
+    assert 0 <= lag < n - L + 1
+    assert val == pytest.approx(L, rel=1e-4)         # |c| = L everywhere
+    assert dt < 0.5

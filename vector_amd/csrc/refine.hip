@@ -10,10 +10,14 @@
 // pass re-ranks, in double precision and in the caller's operand precision
 // (complex64 or complex128), every output whose fp32 |c| lies within a band
 // eps of the fp32 maximum:
-//   select  : candidate items -- the waves of the fused correlator whose
-//             partial max is in the band (a wave covers the outputs
-//             ob + 64 w + l + stride q, l < 64, q < Q, see xcorr.hip), or the
-//             64-output chunks of a stored c64 array holding one;
+//   select  : candidate items -- for the fused correlator, fused with the
+//             finalize of its wave partials into one launch (the last block
+//             to finish reduces, then selects): the thread columns whose lane
+//             key is in the band (64 outputs m(t) + TF q of one thread, where
+//             the kernel writes lane keys), else the waves whose partial max
+//             is (a wave covers ob + wstep w + l + 64 (q % rsub) + stride
+//             (q / rsub), see xcorr.hip); for a stored c64 array, its
+//             64-output chunks holding one;
 //   stage 1 : every output of every item by a plain fp64 direct sum
 //             c[o] = sum_k a[i - (nv-1) + k] conj(v[k]), i = F + o (the same
 //             formula numpy evaluates), max |c|^2 by a 64-bit atomic max;
@@ -21,11 +25,13 @@
 //             dot product (Ogita-Rump-Oishi Dot2: TwoProd by FMA + TwoSum,
 //             as accurate as a 2x-precision sum rounded once), then the max
 //             |c|^2 and the lowest output index attaining it (np.argmax's
-//             first-max rule);
-//   finish  : the peak record's max / index replaced (sums untouched);
-//             optionally the refined values patched into a complex128 c.
+//             first-max rule) by the last stage-2 block, which replaces the
+//             peak record's max / index (sums untouched);
+//   patch   : optionally the refined values into a complex128 c.
 // All sizes on the device (no host synchronisation); more than `cap` items
 // leaves the record as the fp32 pass produced it and sets status = 1.
+// Cross-block hand-offs (last block to finish) use one agent-scope fence per
+// block and agent-scope atomic loads of what other blocks wrote.
 #include "os_common.hpp"
 
 namespace vsig {
@@ -65,7 +71,7 @@ __device__ __forceinline__ void tap_range(long long i, long long na, long long n
   k1 = hi < nv ? hi : nv;
 }
 
-// Shared scratch header (zeroed by the host before select).
+// Shared scratch header (zeroed before select: by the fused finalize, or a memset).
 struct RefineKeys {
   unsigned long long count;    // candidate items appended by select
   unsigned long long max1;     // bits of the stage-1 max |c|^2 (>= 0: integer order)
@@ -80,19 +86,6 @@ static_assert(sizeof(RefineKeys) <= 64, "the items follow the keys at +64 B");
 __device__ __forceinline__ double band_threshold(const PeakPartial* rec, double eps) {
   const double t = rec->max2 * (1.0 - eps);     // finalized record: max |c|
   return t > 0.0 ? t : 0.0;
-}
-
-__global__ __launch_bounds__(256) void refine_select_partials(
-    const PeakPartial* __restrict__ parts, long long nparts, const PeakPartial* __restrict__ rec,
-    double eps, long long cap, long long* __restrict__ items, RefineKeys* __restrict__ keys) {
-  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= nparts) return;
-  const double t = band_threshold(rec, eps);
-  if (parts[p].max2 >= t * t) {                 // partials hold fp32 |c|^2
-    const unsigned long long j = atomicAdd(&keys->count, 1ull);
-    if ((long long)j < cap) items[j] = p;
-    else atomicOr(&keys->status, 1ull);
-  }
 }
 
 __global__ __launch_bounds__(256) void refine_select_array(
@@ -204,6 +197,9 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     for (long long pb = lo + (tid - lane); pb < hi; pb += 256) {   // uniform per wave
       const long long p = pb + lane;
       unsigned long long hits = __ballot(p < hi && f.parts[p].max2 >= t2);
+      // past the cap the refine is skipped anyway (status 1): stop appending
+      // (a flat |c| puts every partial in the band)
+      if (*(volatile unsigned long long*)&scount > (unsigned long long)f.cap) hits = 0;
       while (hits) {
         const int src = __builtin_ctzll(hits);
         hits &= hits - 1;
@@ -225,6 +221,8 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
         if (take && (long long)j < f.cap) f.items[j] = item;
       }
     }
+    __syncthreads();
+    if (scount > (unsigned long long)f.cap) break;   // uniform
   }
   __syncthreads();
   if (tid == 0) {
@@ -565,15 +563,12 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
     if (r.cols || r.lkeys) return hipErrorInvalidValue;
     hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
     if (e != hipSuccess) return e;
-    if (r.from_array) {
-      const long long grid = (r.nout + 255) / 256;
-      hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
-                         rec, r.eps, r.cap_items, items, keys);
-    } else {
-      const long long grid = (r.nparts + 255) / 256;
-      hipLaunchKernelGGL(refine_select_partials, dim3((unsigned)grid), dim3(256), 0, st, r.parts,
-                         r.nparts, rec, r.eps, r.cap_items, items, keys);
-    }
+    // a stored c64 array (the correlator's partials are finalized and
+    // selected by refine_finalize_select above)
+    if (!r.from_array) return hipErrorInvalidValue;
+    const long long grid = (r.nout + 255) / 256;
+    hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
+                       rec, r.eps, r.cap_items, items, keys);
   }
   // stage grids (grid-stride over the device-side candidate count): stage 1
   // 64 / OUTS blocks per unit, stage 2 one block per 64 entries, capped so
