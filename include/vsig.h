@@ -100,7 +100,10 @@ int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
 /* Outcome of the context's last refine pass (synchronises the stream):
  * status 0 refined, 1 skipped (more candidates than refine_cap), 2 no pass
- * ran (refine off, or no correlation yet); candidates = candidate items. */
+ * ran (refine off, or no correlation yet); candidates = candidate items
+ * (64-output thread columns of the M = 16384 / 32768 correlators, waves of the
+ * M = 4096 / 8192 ones, 64-output chunks of a stored array; past the cap the
+ * count stops near refine_cap / 64 items). */
 int vsig_refine_status(vsig_ctx* ctx, int32_t* status, int64_t* candidates);
 /* Hash of the kernel / ABI sources this library was built from (the Python
  * loader compares it with the sources next to it and refuses a stale build). */
