@@ -177,9 +177,14 @@ class StreamChain:
         self.x_ext = backend.empty(self.hist + cfg.n_local)          # [left halo | chunk]
         self.y_ext = backend.empty(self.ny + max(self.L - 1, 0))     # [chunk out | right halo]
         self.sxx = backend.empty((self.ny // cfg.nfft) * cfg.nfft, torch.float32)
-        self.recs = backend.empty(4 * cfg.pipeline, torch.float64).view(cfg.pipeline, 4)
-        # every rank's records, gathered in place (one collective, no copies)
-        self.rows = backend.empty(4 * cfg.pipeline * world, torch.float64).view(world * cfg.pipeline, 4)
+        # peak records, double-buffered: the all-gather of step k runs behind
+        # step k + 1 (it is waited for only before step k + 2 reuses its slot,
+        # or by global_peak); every rank's records land in place (no copies)
+        K = cfg.pipeline
+        self._recs = backend.empty(2 * 4 * K, torch.float64).view(2, K, 4)
+        self._rows = backend.empty(2 * 4 * K * world, torch.float64).view(2, world * K, 4)
+        self._gather = [None, None]
+        self._slot = 1
         self.peak_rows = None
 
     @property
@@ -191,9 +196,22 @@ class StreamChain:
     def y(self):
         return self.y_ext[: self.ny]
 
+    @property
+    def recs(self):
+        """This step's peak records (one per sub-chunk)."""
+        return self._recs[self._slot]
+
+    def _begin_step(self):
+        self._slot ^= 1
+        work, self._gather[self._slot] = self._gather[self._slot], None
+        if work is not None:              # the all-gather two steps back (long done)
+            work.wait()
+
     def _gather_peaks(self):
-        dist.all_gather_into_tensor(self.rows, self.recs, group=self.group)
-        return list(self.rows.view(self.world, self.cfg.pipeline, 4).unbind(0))
+        rows = self._rows[self._slot]
+        self._gather[self._slot] = dist.all_gather_into_tensor(rows, self.recs, group=self.group,
+                                                               async_op=True)
+        return list(rows.view(self.world, self.cfg.pipeline, 4).unbind(0))
 
     def _exchange_start(self, send, dst, recv, src):
         ops = []
@@ -243,6 +261,7 @@ class StreamChain:
         run(0, min(s, nk))
 
     def step(self):
+        self._begin_step()
         if self.cfg.serial:
             return self._step_serial()
         if self.cfg.pipeline == 1 and self.cfg.one_stream:
@@ -354,6 +373,9 @@ class StreamChain:
 
     def global_peak(self):
         """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step."""
+        work = self._gather[self._slot]
+        if work is not None:
+            work.wait()
         rows = []
         nyk = self.ny // self.cfg.pipeline
         for r, t in enumerate(self.peak_rows):
