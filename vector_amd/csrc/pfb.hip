@@ -51,66 +51,74 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
     const long long i = m * C + p;
     return i < n ? x[i] : make_float2(0.f, 0.f);
   };
-  float2 ring[PT];
-#pragma unroll
-  for (int q = 0; q < PT - 1; ++q) ring[q] = row(m0 + q);
   constexpr bool PF = (VAR & 2) != 0;
-  float2 nxt[PF ? E : 1];
-  if constexpr (PF) {
-#pragma unroll
-    for (int i = 0; i < E; ++i) nxt[i] = row(m0 + PT - 1 + i);
-  }
   // FFT role of this thread: frame slot ff of the batch, thread t of the frame
   const int ff = tid / TF, t = tid % TF;
-  const long long mout0 = (blk * G + ff / E) * fpg + ff % E;
   float2* fl = lds + ff * PL::LDS;
-  for (long long b = 0; b < fpg; b += (long long)E * U) {
-    static_for<0, U>([&](auto ui) {
-      constexpr int u = decltype(ui)::value;
-      static_for<0, E>([&](auto ii) {
-        constexpr int i = decltype(ii)::value;
-        constexpr int k = u * E + i;                          // frame index mod ring
-        const long long m = m0 + b + k;
-        if constexpr (PF) ring[(k + PT - 1) % PT] = nxt[i];
-        else ring[(k + PT - 1) % PT] = row(m + PT - 1);
-        float2 z = make_float2(0.f, 0.f);
-        static_for<0, PT>([&](auto qi) {
-          constexpr int q = decltype(qi)::value;
-          z.x = fmaf(hq[q], ring[(k + q) % PT].x, z.x);
-          z.y = fmaf(hq[q], ring[(k + q) % PT].y, z.y);
-        });
-        lds[(g * E + i) * PL::LDS + lpad(p)] = z;
-      });
-      if constexpr (PF) {
-        const long long mn = m0 + b + (u + 1) * E + PT - 1;   // next batch's new rows
+  // Odd groups walk their frames backwards: the PT - 1 rows two neighbouring
+  // groups share are then read by both at the same time (both walks start, or
+  // both end, there), so the second read is an L2 hit instead of a re-fetch
+  // from HBM one whole walk later.  Walk step f is frame mf(f); its new row is
+  // the frame's last row (forward) or first row (backward); ring slot of row
+  // mf(f) + q: (f + q) % PT forward, (f + PT - 1 - q) % PT backward.
+  auto walk = [&](auto bwdc) {
+    constexpr bool BWD = decltype(bwdc)::value;
+    auto mf = [&](long long f) { return BWD ? m0 + fpg - 1 - f : m0 + f; };
+    auto newrow = [&](long long f) { return BWD ? mf(f) : mf(f) + PT - 1; };
+    float2 ring[PT];
 #pragma unroll
-        for (int i = 0; i < E; ++i) nxt[i] = row(mn + i);
-      }
-      __syncthreads();
-      float2 v[E];
-      fft_load<PL, 0>(v, fl, t);
-      fft_frame<PL>(v, fl, tw, t);
-      if constexpr (VAR & 1) {
+    for (int q = 1; q < PT; ++q)                      // rows of frame mf(0) but its new one
+      ring[BWD ? PT - 1 - q : q - 1] = row(mf(0) + (BWD ? q : q - 1));
+    float2 nxt[PF ? E : 1];
+    if constexpr (PF) {
+#pragma unroll
+      for (int i = 0; i < E; ++i) nxt[i] = row(newrow(i));
+    }
+    for (long long b = 0; b < fpg; b += (long long)E * U) {
+      static_for<0, U>([&](auto ui) {
+        constexpr int u = decltype(ui)::value;
+        static_for<0, E>([&](auto ii) {
+          constexpr int i = decltype(ii)::value;
+          constexpr int k = u * E + i;                        // walk step mod ring period
+          if constexpr (PF) ring[(k + PT - 1) % PT] = nxt[i];
+          else ring[(k + PT - 1) % PT] = row(newrow(b + k));
+          float2 z = make_float2(0.f, 0.f);
+          static_for<0, PT>([&](auto qi) {
+            constexpr int q = decltype(qi)::value;
+            constexpr int slot = BWD ? (k + PT - 1 - q) % PT : (k + q) % PT;
+            z.x = fmaf(hq[q], ring[slot].x, z.x);
+            z.y = fmaf(hq[q], ring[slot].y, z.y);
+          });
+          lds[(g * E + i) * PL::LDS + lpad(p)] = z;
+        });
+        if constexpr (PF) {
+#pragma unroll
+          for (int i = 0; i < E; ++i) nxt[i] = row(newrow(b + (u + 1) * E + i));   // next batch
+        }
+        __syncthreads();
+        float2 v[E];
+        fft_load<PL, 0>(v, fl, t);
+        fft_frame<PL>(v, fl, tw, t);
+        static_assert(VAR & 1, "the walk directions need the LDS-staged stores");
         __syncthreads();                                      // last FFT pass read lds
 #pragma unroll
         for (int e = 0; e < E; ++e) fl[lpad(out_index<PL>(t, e))] = v[e];
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < E; ++i) {
-          const long long m = m0 + b + u * E + i;
+          const long long m = mf(b + u * E + i);
           if (m < M) y[m * C + p] = lds[(g * E + i) * PL::LDS + lpad(p)];
         }
-      } else {
-        const long long m = mout0 + b + u * E;
-        if (m < M) {
-          float2* yo = y + m * C;
-#pragma unroll
-          for (int e = 0; e < E; ++e) yo[out_index<PL>(t, e)] = v[e];
-        }
-      }
-      __syncthreads();                                        // lds reused by the next batch
-    });
-  }
+        __syncthreads();                                      // lds reused by the next batch
+      });
+    }
+  };
+#ifdef VSIG_PFB_FWD_ONLY        // tuning builds: every group walks forward
+  walk(IC<0>{});
+#else
+  if (gid & 1) walk(IC<1>{});
+  else walk(IC<0>{});
+#endif
 }
 
 // Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3),
