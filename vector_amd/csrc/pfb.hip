@@ -25,6 +25,13 @@ namespace vsig {
 
 constexpr int cgcd(int a, int b) { return b == 0 ? a : cgcd(b, a % b); }
 
+// a + hp.x * u (HI = 0) or a + hp.y * u (HI = 1), both halves of u: one
+// v_pk_fma_f32 with the tap broadcast by op_sel / op_sel_hi
+template <int HI>
+__device__ __forceinline__ f2v tap_fma(f2v hp, f2v u, f2v a) {
+  return __builtin_elementwise_fma(HI ? hp.yy : hp.xx, u, a);
+}
+
 // VAR bit 0: spectra leave through LDS so every store is a full C-point row
 // (512 B per wave instruction for C = 64) instead of TF-point runs.
 // VAR bit 1: the next batch's E input rows are loaded before this batch's FFT
@@ -41,15 +48,26 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
   static_assert(G * E * TF == 256, "one FFT thread per (frame, t) of a batch");
   __shared__ float2 lds[G * E * PL::LDS];
   const int tid = threadIdx.x, p = tid % C, g = tid / C;
-  float hq[PT];
+  // taps in pairs (h[2j C + p], h[(2j + 1) C + p]): one packed FMA per tap
+  // with the pair's low / high half broadcast through op_sel
+  static_assert(PT % 2 == 0, "tap pairs");
+  f2v hq2[PT / 2];
 #pragma unroll
-  for (int q = 0; q < PT; ++q) hq[q] = h[q * C + p];
+  for (int j = 0; j < PT / 2; ++j) hq2[j] = (f2v){h[2 * j * C + p], h[(2 * j + 1) * C + p]};
   const long long blk = xcd_remap(blockIdx.x, gridDim.x);   // contiguous runs per XCD
   const long long gid = blk * G + g;                          // this lane's group
   const long long m0 = gid * fpg;
-  auto row = [&](long long m) -> float2 {                     // x[m*C + p] or 0
-    const long long i = m * C + p;
-    return i < n ? x[i] : make_float2(0.f, 0.f);
+  // rows by offset r from the group's first frame: x[(m0 + r) C + p], bounds-
+  // checked (zero past n) only in the walks that reach the end of the stream
+  const float2* xg = x + m0 * C + p;
+  const bool inside = (m0 + fpg + PT - 1) * C <= n;          // wave-uniform
+  auto row = [&](long long r, auto chkc) -> float2 {
+    if constexpr (decltype(chkc)::value) {
+      const long long i = (m0 + r) * C + p;
+      return i < n ? x[i] : make_float2(0.f, 0.f);
+    } else {
+      return xg[(int)r * C];
+    }
   };
   constexpr bool PF = (VAR & 2) != 0;
   // FFT role of this thread: frame slot ff of the batch, thread t of the frame
@@ -61,18 +79,19 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
   // from HBM one whole walk later.  Walk step f is frame mf(f); its new row is
   // the frame's last row (forward) or first row (backward); ring slot of row
   // mf(f) + q: (f + q) % PT forward, (f + PT - 1 - q) % PT backward.
-  auto walk = [&](auto bwdc) {
+  auto walk = [&](auto bwdc, auto chkc) {
     constexpr bool BWD = decltype(bwdc)::value;
-    auto mf = [&](long long f) { return BWD ? m0 + fpg - 1 - f : m0 + f; };
-    auto newrow = [&](long long f) { return BWD ? mf(f) : mf(f) + PT - 1; };
+    auto rf = [&](long long f) { return BWD ? fpg - 1 - f : f; };     // frame offset
+    auto mf = [&](long long f) { return m0 + rf(f); };
+    auto newrow = [&](long long f) { return BWD ? rf(f) : rf(f) + PT - 1; };
     float2 ring[PT];
 #pragma unroll
     for (int q = 1; q < PT; ++q)                      // rows of frame mf(0) but its new one
-      ring[BWD ? PT - 1 - q : q - 1] = row(mf(0) + (BWD ? q : q - 1));
+      ring[BWD ? PT - 1 - q : q - 1] = row(rf(0) + (BWD ? q : q - 1), chkc);
     float2 nxt[PF ? E : 1];
     if constexpr (PF) {
 #pragma unroll
-      for (int i = 0; i < E; ++i) nxt[i] = row(newrow(i));
+      for (int i = 0; i < E; ++i) nxt[i] = row(newrow(i), chkc);
     }
     for (long long b = 0; b < fpg; b += (long long)E * U) {
       static_for<0, U>([&](auto ui) {
@@ -81,19 +100,18 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
           constexpr int i = decltype(ii)::value;
           constexpr int k = u * E + i;                        // walk step mod ring period
           if constexpr (PF) ring[(k + PT - 1) % PT] = nxt[i];
-          else ring[(k + PT - 1) % PT] = row(newrow(b + k));
-          float2 z = make_float2(0.f, 0.f);
-          static_for<0, PT>([&](auto qi) {
+          else ring[(k + PT - 1) % PT] = row(newrow(b + k), chkc);
+          f2v z[2] = {(f2v){0.f, 0.f}, (f2v){0.f, 0.f}};   // even / odd taps: no
+          static_for<0, PT>([&](auto qi) {                    // back-to-back dependence
             constexpr int q = decltype(qi)::value;
             constexpr int slot = BWD ? (k + PT - 1 - q) % PT : (k + q) % PT;
-            z.x = fmaf(hq[q], ring[slot].x, z.x);
-            z.y = fmaf(hq[q], ring[slot].y, z.y);
+            z[q & 1] = tap_fma<q & 1>(hq2[q / 2], tov(ring[slot]), z[q & 1]);
           });
-          lds[(g * E + i) * PL::LDS + lpad(p)] = z;
+          lds[(g * E + i) * PL::LDS + lpad(p)] = fromv(z[0] + z[1]);
         });
         if constexpr (PF) {
 #pragma unroll
-          for (int i = 0; i < E; ++i) nxt[i] = row(newrow(b + (u + 1) * E + i));   // next batch
+          for (int i = 0; i < E; ++i) nxt[i] = row(newrow(b + (u + 1) * E + i), chkc);   // next batch
         }
         __syncthreads();
         float2 v[E];
@@ -114,15 +132,24 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
     }
   };
 #ifdef VSIG_PFB_FWD_ONLY        // tuning builds: every group walks forward
-  walk(IC<0>{});
+  if (inside) walk(IC<0>{}, IC<0>{});
+  else walk(IC<0>{}, IC<1>{});
 #else
-  if (gid & 1) walk(IC<1>{});
-  else walk(IC<0>{});
+  if (gid & 1) {
+    if (inside) walk(IC<1>{}, IC<0>{});
+    else walk(IC<1>{}, IC<1>{});
+  } else {
+    if (inside) walk(IC<0>{}, IC<0>{});
+    else walk(IC<0>{}, IC<1>{});
+  }
 #endif
 }
 
-// Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3),
-// 64 frames per group.
+// Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3;
+// C = 64: registers capped for 4 waves / SIMD, VAR 7), 64 frames per group.
+#ifndef VSIG_PFB_VAR64
+#define VSIG_PFB_VAR64 7
+#endif
 template <class PL, int PT>
 static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
                          const float2* tw, hipStream_t st) {
@@ -137,7 +164,7 @@ static void launch_pfb_t(const float2* x, long long n, const float* h, long long
   const long long fpg = ((want + step - 1) / step) * step;
   const long long groups = (M + fpg - 1) / fpg;
   const long long blocks = (groups + G - 1) / G;
-  hipLaunchKernelGGL((pfb_kernel<PL, PT, 3>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M,
+  hipLaunchKernelGGL((pfb_kernel<PL, PT, PL::N == 64 ? VSIG_PFB_VAR64 : 3>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M,
                      fpg, y, tw);
 }
 
