@@ -59,9 +59,9 @@ __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
           const int i = 2 * t + S0 * r;
           const f4 q = active ? __builtin_nontemporal_load(reinterpret_cast<const f4*>(xf + i))
                               : f4{0.f, 0.f, 0.f, 0.f};
-          const float2 w2 = *reinterpret_cast<const float2*>(win + i);
-          v[f][r] = make_float2(q.x * w2.x, q.y * w2.x);
-          v[f][R0 + r] = make_float2(q.z * w2.y, q.w * w2.y);
+          const f2v w2 = *reinterpret_cast<const f2v*>(win + i);   // packed: window broadcast
+          v[f][r] = fromv((f2v){q.x, q.y} * w2.xx);
+          v[f][R0 + r] = fromv((f2v){q.z, q.w} * w2.yy);
         }
       }
     }
