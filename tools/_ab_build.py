@@ -20,6 +20,7 @@ VARIANTS = {
     "libvsig_ilv61": ("VSIG_ILV_S=6", "VSIG_ILV_U=1"),
     "libvsig_pfbfwd": ("VSIG_PFB_FWD_ONLY",),
     "libvsig_pfbv3": ("VSIG_PFB_VAR64=3",),
+    "libvsig_nobufld": ("VSIG_NO_BUFLD",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

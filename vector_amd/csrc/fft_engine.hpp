@@ -784,6 +784,19 @@ __device__ __forceinline__ int out_index(int t, int e) {         // result e of 
   constexpr int R = P::RL;
   return bfly<P, P::NP - 1>(t, e / R) + (e % R) * (P::N / R);
 }
+// in_index(t, e) - in_index(t, 0) and out_index(t, e) - out_index(t, 0): the
+// same for every thread under the lane maps other than kMapIlv (one per-lane
+// base address plus compile-time offsets per element)
+template <class P>
+constexpr int in_off(int e) {
+  static_assert(map0_of<P>::value != kMapIlv, "per-lane constant offsets");
+  return (e / P::R[0]) * P::TF + (e % P::R[0]) * (P::N / P::R[0]);
+}
+template <class P>
+constexpr int out_off(int e) {
+  static_assert(mapl_of<P>::value != kMapIlv, "per-lane constant offsets");
+  return (e / P::RL) * P::TF + (e % P::RL) * (P::N / P::RL);
+}
 
 // ---------------------------------------------------------------------------
 // The plans instantiated by the library (N -> elements/thread, radices).

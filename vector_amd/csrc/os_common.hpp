@@ -28,6 +28,26 @@ __device__ __forceinline__ void st_stream(float2* p, float2 v) {
 // Pass-0 operands of an overlap-save segment x[s0 .. s0 + N) with zero fill
 // outside [0, n).  The block-uniform base keeps the address in SGPRs; interior
 // segments (the common case) skip the per-element bounds test.
+// Raw buffer loads with a wave-uniform descriptor: the per-lane part of the
+// address is one 32-bit voffset shared by all of a thread's loads, the
+// per-element constants go to soffset (SGPRs), so a burst of loads costs no
+// 64-bit address arithmetic (v_add_co / v_addc pairs and their wait states).
+// The descriptor inputs pass readfirstlane so the compiler sees them uniform.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, unsigned bytes) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  void* q = reinterpret_cast<void*>(((unsigned long long)hi << 32) | lo);
+  return __builtin_amdgcn_make_buffer_rsrc(q, (short)0, (int)__builtin_amdgcn_readfirstlane(bytes),
+                                           0x00020000);
+}
+__device__ __forceinline__ float2 buf_load2(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, (int)voff, soff, 0));
+}
+__device__ __forceinline__ float4 buf_load4(__amdgpu_buffer_rsrc_t r, unsigned voff, int soff) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, (int)voff, soff, 0));
+}
+
 template <class P, bool NT = false>
 __device__ __forceinline__ void load_segment(float2* v, const float2* __restrict__ x,
                                              long long s0, long long n, int t) {

@@ -177,6 +177,18 @@ __device__ __forceinline__ void load_halves(float2* a, float2* d, const float2* 
     }
   }
   if (s0 >= 0 && s0 + 2 * H <= n) {
+#ifndef VSIG_NO_BUFLD
+    if constexpr (!plan_ilv<P>()) {   // one voffset per thread, the rest in soffset
+      const auto rs = make_rsrc(base, 2u * H * (unsigned)sizeof(float2));
+      const unsigned v0 = (unsigned)in_index<P>(t, 0) * (unsigned)sizeof(float2);
+      static_for<0, P::E>([&](auto ei) {
+        constexpr int e = decltype(ei)::value;
+        a[e] = buf_load2(rs, v0, in_off<P>(e) * (int)sizeof(float2));
+        d[e] = buf_load2(rs, v0, (in_off<P>(e) + H) * (int)sizeof(float2));
+      });
+      return;
+    }
+#endif
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const unsigned i = (unsigned)in_index<P>(t, e);
@@ -368,11 +380,25 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
     d[e] = twc<half_root<P, M>(e), 64>(cmul(csub(x0, x1), (plan_ilv<P>() && e >= P::R[0]) ? w1 : w));
   });
   fft2(a, d);
+#ifndef VSIG_NO_BUFLD
+  if constexpr (!plan_ilv<P>()) {
+    const auto rp = make_rsrc(Ps2, (unsigned)P::N * (unsigned)sizeof(float4));
+    const unsigned v0 = (unsigned)out_index<P>(t, 0) * (unsigned)sizeof(float4);
+    static_for<0, P::E>([&](auto ei) {
+      constexpr int e = decltype(ei)::value;
+      const float4 p = buf_load4(rp, v0, out_off<P>(e) * (int)sizeof(float4));
+      a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
+      d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
+    });
+  } else
+#endif
+  {
 #pragma unroll
-  for (int e = 0; e < P::E; ++e) {
-    const float4 p = Ps2[out_index<P>(t, e)];
-    a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
-    d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
+    for (int e = 0; e < P::E; ++e) {
+      const float4 p = Ps2[out_index<P>(t, e)];
+      a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
+      d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
+    }
   }
   fft2(a, d);
   static_for<0, P::E>([&](auto ei) {
