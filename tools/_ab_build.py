@@ -21,6 +21,7 @@ VARIANTS = {
     "libvsig_pfbfwd": ("VSIG_PFB_FWD_ONLY",),
     "libvsig_pfbv3": ("VSIG_PFB_VAR64=3",),
     "libvsig_nobufld": ("VSIG_NO_BUFLD",),
+    "libvsig_unphased": ("VSIG_FFT_UNPHASED",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

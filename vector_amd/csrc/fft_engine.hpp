@@ -53,6 +53,13 @@ __device__ __forceinline__ float2 cmul(float2 a, float2 b) {
       : "=v"(r) : "v"(av), "v"(bv), "v"(t));
   return fromv(r);
 }
+// cmul(a, b) given t = a * b.xx (so that the two halves can be scheduled apart)
+__device__ __forceinline__ float2 cmul_fin(float2 a, float2 b, f2v t) {
+  f2v r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0]"
+      : "=v"(r) : "v"(tov(a)), "v"(tov(b)), "v"(t));
+  return fromv(r);
+}
 // a + (-i) b = (a.x + b.y, a.y - b.x)   and   a - (-i) b = (a.x - b.y, a.y + b.x)
 __device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) {
   f2v r;
@@ -76,9 +83,9 @@ __device__ __forceinline__ float2 cfma_s(float2 u, float h, float2 a) {
 // b * (c - i s) for compile-time c, s: c * (b.x, b.y) + s * (b.y, -b.x)
 __device__ __forceinline__ float2 cmul_cs(float2 b, float c, float s_) {
   const f2v bv = tov(b);
-  const f2v cc = (f2v){c, c}, ss = (f2v){s_, s_};
-  f2v t, r;
-  asm("v_pk_mul_f32 %0, %1, %2" : "=v"(t) : "v"(bv), "s"(cc));
+  const f2v ss = (f2v){s_, s_};
+  const f2v t = bv * (f2v){c, c};       // plain product: the compiler schedules it
+  f2v r;
   asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
       : "=v"(r) : "v"(bv), "s"(ss), "v"(t));
   return fromv(r);
@@ -120,6 +127,13 @@ constexpr float kSin64[32] = {
     7.071067812e-01f, 6.343932842e-01f, 5.555702330e-01f, 4.713967368e-01f,
     3.826834324e-01f, 2.902846773e-01f, 1.950903220e-01f, 9.801714033e-02f};
 
+// Compile-time loop: f(IC<B>{}) ... f(IC<E - 1>{}).
+template <int I> struct IC { static constexpr int value = I; };
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) { f(IC<B>{}); static_for<B + 1, E>(f); }
+}
+
 // b * exp(-2*pi*i*K/M) with compile-time K, M (M <= 64).  Trivial factors
 // (1, -i, and the 45-degree family) are special-cased so they cost no multiply.
 template <int K, int M>
@@ -141,7 +155,88 @@ __device__ __forceinline__ float2 twc(float2 b) {
   }
 }
 
-// One radix-2 Stockham step inside registers: Ns = 2^P.
+// One radix-2 Stockham step inside registers: Ns = 2^P.  The step runs in
+// three phases over all its butterflies J -- (A) the first half of every
+// twiddle product, (B) the second half, (C) the sums -- so that a packed op
+// and its consumer are never adjacent: gfx950 needs one wait state between a
+// packed fp32 op and a dependent one, and hipcc pads every inline-asm
+// boundary with one, while independent work in between costs nothing.
+#ifndef VSIG_FFT_UNPHASED
+template <int R, int P>
+struct Radix2Phased {
+  static constexpr int Ns = 1 << P, M = 2 * Ns;
+  template <int J> static constexpr int kk() { return J & (Ns - 1); }
+  template <int J> static constexpr bool general() {
+    constexpr int k = kk<J>();
+    return k != 0 && 4 * k != M && 8 * k != M && 8 * k != 3 * M;
+  }
+  __device__ __forceinline__ static void run(const float2* a, float2* t) {
+    float2 u[R / 2];
+    // (A) general twiddles: b * cos; 45-degree family: (b.x +- b.y, ...)
+    static_for<0, R / 2>([&](auto ji) {
+      constexpr int J = decltype(ji)::value;
+      constexpr int k = kk<J>();
+      const float2 b = a[J + R / 2];
+      if constexpr (general<J>()) {
+        constexpr int idx = k * (64 / M);
+#ifdef VSIG_PK
+        u[J] = fromv(tov(b) * (f2v){kCos64[idx], kCos64[idx]});
+#else
+        u[J] = b;
+#endif
+      } else if constexpr (8 * k == M) {
+        u[J] = cadd_mi(b, b);
+      } else if constexpr (8 * k == 3 * M) {
+        u[J] = csub_mi(b, b);
+      }
+    });
+    // (B) general twiddles: + sin * (b.y, -b.x)
+    static_for<0, R / 2>([&](auto ji) {
+      constexpr int J = decltype(ji)::value;
+      if constexpr (general<J>()) {
+        constexpr int idx = kk<J>() * (64 / M);
+        const float2 b = a[J + R / 2];
+#ifdef VSIG_PK
+        const f2v bv = tov(b), ss = (f2v){kSin64[idx], kSin64[idx]};
+        f2v r;
+        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+            : "=v"(r) : "v"(bv), "s"(ss), "v"(tov(u[J])));
+        u[J] = fromv(r);
+#else
+        u[J] = cmul_cs(b, kCos64[idx], kSin64[idx]);
+#endif
+      }
+    });
+    // (C) the butterflies' sums
+    static_for<0, R / 2>([&](auto ji) {
+      constexpr int J = decltype(ji)::value;
+      constexpr int k = kk<J>();
+      constexpr int o = ((J >> P) << (P + 1)) + k;
+      const float2 x0 = a[J];
+      const float2 b = a[J + R / 2];
+      if constexpr (k == 0) {
+        t[o] = cadd(x0, b);
+        t[o + Ns] = csub(x0, b);
+      } else if constexpr (4 * k == M) {           // (-i) b folded into the adds
+        t[o] = cadd_mi(x0, b);
+        t[o + Ns] = csub_mi(x0, b);
+      } else if constexpr (8 * k == M) {           // h (b.x + b.y, b.y - b.x)
+        constexpr float h = 7.071067812e-01f;
+        t[o] = cfma_s(u[J], h, x0);
+        t[o + Ns] = cfma_s(u[J], -h, x0);
+      } else if constexpr (8 * k == 3 * M) {       // -h (b.x - b.y, b.x + b.y)
+        constexpr float h = 7.071067812e-01f;
+        t[o] = cfma_s(u[J], -h, x0);
+        t[o + Ns] = cfma_s(u[J], h, x0);
+      } else {
+        t[o] = cadd(x0, u[J]);
+        t[o + Ns] = csub(x0, u[J]);
+      }
+    });
+  }
+};
+#endif
+
 template <int R, int P, int J>
 struct Radix2Step {
   __device__ __forceinline__ static void run(const float2* a, float2* t) {
@@ -180,7 +275,11 @@ template <int R, int P>
 struct DftPasses {
   __device__ __forceinline__ static void run(float2* v) {
     float2 t[R];
+#ifndef VSIG_FFT_UNPHASED
+    Radix2Phased<R, P>::run(v, t);
+#else
     Radix2Step<R, P, 0>::run(v, t);
+#endif
 #pragma unroll
     for (int i = 0; i < R; ++i) v[i] = t[i];
     if constexpr ((2 << P) < R) DftPasses<R, P + 1>::run(v);
@@ -364,13 +463,6 @@ __device__ __forceinline__ int opaque_zero() {
   return z;
 }
 
-// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E).
-template <int I> struct IC { static constexpr int value = I; };
-template <int B, int E, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (B < E) { f(IC<B>{}); static_for<B + 1, E>(f); }
-}
-
 // Twiddle sources for passes p >= 1.
 //  TwTable  : the global per-plan table (one load per element and pass).
 //  TwAnchors: per-thread register anchors w^a, a in {1, 8, 16, 24} (< R), read
@@ -499,11 +591,29 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
     const float2* wa = tws.wa + anch_off<P>(p) + b * NA;
     const float2 w1 = wa[0];
     float2 cur = w1;
+#if defined(VSIG_PK) && !defined(VSIG_FFT_UNPHASED)
+    // software-pipelined by one power: the next power's product and this
+    // element's product alternate, so no packed op is followed by its
+    // dependent (one wait state each otherwise, see Radix2Phased)
+    static_for<1, R>([&](auto ri) {
+      constexpr int r = decltype(ri)::value;
+      constexpr bool adv = r + 1 < R && (r + 1) % 8 != 0;
+      f2v tc;
+      if constexpr (adv) tc = tov(cur) * tov(w1).xx;
+      const f2v tv = tov(v[b * R + r]) * tov(cur).xx;
+      float2 nxt = cur;
+      if constexpr (adv) nxt = cmul_fin(cur, w1, tc);
+      else if constexpr (r + 1 < R) nxt = wa[(r + 1) / 8];
+      v[b * R + r] = cmul_fin(v[b * R + r], cur, tv);
+      cur = nxt;
+    });
+#else
 #pragma unroll
     for (int r = 1; r < R; ++r) {
       if (r > 1) cur = (r % 8 == 0) ? wa[r / 8] : cmul(cur, w1);
       v[b * R + r] = cmul(v[b * R + r], cur);
     }
+#endif
   }
 }
 
