@@ -126,6 +126,20 @@ def xcorr_block(L):
     return 4096 if L <= 1024 else 8192 if L <= 2048 else 16384
 
 
+def practical_ceiling(kind):
+    """The best rate the pool's boxes reached on an access pattern like the
+    kernel's (tools/membw.py probes, profiles/r02_membw.json): 'read4to1' for
+    the decimating FIR's 8 B read : 2 B written per sample, 'copy' (16-byte
+    lanes, loads in flight, NT hints) for the 1:1 streams.  (GB/s, source)"""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "r02_membw.json")))
+    except Exception:
+        return None
+    pref = "read4to1" if kind == "read4to1" else "probe_u"
+    vals = [v[1] for k, v in d.items() if k.startswith(pref) and isinstance(v, list)]
+    return (max(vals), f"profiles/r02_membw.json max({pref}*)") if vals else None
+
+
 def load_traffic(key):
     """Measured HBM bytes per launch from a committed rocprofv3 --pmc summary
     (profiles/pmc_*.json, corrected as MI355X_MICROARCH.md §HBM prescribes)."""
@@ -298,6 +312,12 @@ def main():
                 "traffic_source": pmc["source"] if pmc else None}
         if pmc and "valu_issue_frac" in pmc:
             roof["valu_issue_frac"] = pmc["valu_issue_frac"]
+        # the same rate against what a pure stream of this shape reaches on the box
+        pc = practical_ceiling("read4to1" if (dom == "fir" and decim == 4) else "copy")
+        if pc:
+            roof["practical_peak"] = pc[0]
+            roof["practical_frac"] = round(achieved / pc[0], 4)
+            roof["practical_source"] = pc[1]
     # every stage against its own roof: HBM bytes for all three, and for the
     # correlator (not HBM-bound) the FP32 vector roof with the standard
     # 5 N log2 N FFT flop count (2 FFTs + the spectrum multiply per block)
