@@ -575,10 +575,14 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   // that the usual few candidates do not pay for thousands of idle blocks
   const int split = r.cols ? 16 : 4;
   long long units = r.cap_items * r.Q * split;
-  if (units > 1024) units = 1024;
+#ifndef VSIG_REFINE_G1
+#define VSIG_REFINE_G1 256
+#define VSIG_REFINE_G2 64
+#endif
+  if (units > VSIG_REFINE_G1) units = VSIG_REFINE_G1;   // one block per CU
   const unsigned g1 = (unsigned)units;
   long long g2l = n / 64;
-  if (g2l > 256) g2l = 256;
+  if (g2l > VSIG_REFINE_G2) g2l = VSIG_REFINE_G2;
   const unsigned g2 = (unsigned)g2l;
   auto stages = [&](auto tag) {
     using T = decltype(tag);
