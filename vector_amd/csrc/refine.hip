@@ -108,8 +108,8 @@ __global__ __launch_bounds__(256) void refine_select_array(
 // reduces tmp into the record (max |c|), resets the refine keys and selects
 // the candidates: chunks whose max is in the band, their wave partials in the
 // band, and -- with lane keys -- the thread columns of those waves in the
-// band (items p * 64 + l), else the waves (items p).  Replaces the memset,
-// partial_chunks, partial_finalize and refine_select_partials launches.
+// band (items p * 64 + l), else the waves (items p).  One launch where there
+// were four (a keys memset, partial_chunks, partial_finalize, a select).
 struct FinalizeSelect {
   const PeakPartial* parts; long long nparts, chunk;
   PeakPartial* tmp;                 // gridDim.x first-level records
