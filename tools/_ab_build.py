@@ -23,6 +23,7 @@ VARIANTS = {
     "libvsig_nobufld": ("VSIG_NO_BUFLD",),
     "libvsig_unphased": ("VSIG_FFT_UNPHASED",),
     "libvsig_rg1024": ("VSIG_REFINE_G1=1024", "VSIG_REFINE_G2=256"),
+    "libvsig_nol1tw": ("VSIG_NO_L1TW",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)
