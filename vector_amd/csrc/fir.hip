@@ -222,7 +222,7 @@ __device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
 // for the kernel (profiles/r02_v12_ab.txt), i.e. the loads / stores of this
 // access pattern alone run at 5.5 TB/s and the transforms add ~0.45 ms.
 
-template <bool MIX = false, bool X4 = false>
+template <bool MIX = false, bool X4 = false, bool PERSIST = false>
 __global__ __launch_bounds__(64) void fir_poly_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
     long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
@@ -233,15 +233,21 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
   static_assert(P::TF == 64 && P::E == 16 && P::NP == 2 && P::R[1] == 16 && PD::E == 4,
                 "lane layout of the reduce-scatter");
   __shared__ float2 lds[P::LDS];
-  const int t = threadIdx.x;
-  const long long b = xcd_remap(blockIdx.x, gridDim.x);
-  if (2 * b >= nblocks) return;
+  const int t0 = threadIdx.x;
   const long long nloc = n - g0;
-  const int tq = (t & 15) | ((t & 16) << 1) | ((t & 32) >> 1);
+  const int tq0 = (t0 & 15) | ((t0 & 16) << 1) | ((t0 & 32) >> 1);
   float2 wa[nanch_total<P>()];
-  load_anchors<P>(wa, tw, t);
+  load_anchors<P>(wa, tw, t0);
   float2 wr[rtw_total<PD>()];
-  load_rtw<PD>(wr, twd, tq);
+  load_rtw<PD>(wr, twd, tq0);
+  // PERSIST (tuning builds, VSIG_TUNING): a fixed grid walks the segment pairs
+  // (grid-stride), so that a bounded number of waves is resident; the thread
+  // index is opaque per iteration (no hoisted, pinned per-element addresses)
+  for (long long it = PERSIST ? blockIdx.x : 0;; it += gridDim.x) {
+  const long long b = PERSIST ? it : xcd_remap(blockIdx.x, gridDim.x);
+  if (2 * b >= nblocks) return;
+  const int zz = PERSIST ? opaque_zero() : 0;
+  const int t = t0 + zz, tq = tq0 + zz;
   float2 a[P::E], d[P::E];
   if constexpr (MIX) {
     load_segment_mix<P>(a, x, g0 + (2 * b) * hop - lo2, n, t, mix);
@@ -289,6 +295,8 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
       if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, cconj(u[e]));
     }
   }
+  if constexpr (!PERSIST) return;
+  }
 }
 
 // G_k[j] (see fir_poly_kernel) from Hs = FFT_1024(h) / 1024, in double.
@@ -330,6 +338,11 @@ hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const flo
   const MixArgs m = mix ? *mix : MixArgs{};
   if (mix)
     hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+#ifdef VSIG_TUNING
+  else if (g_tune_fir_grid > 0 && x4_aligned(x, g0 - lo2, hop))
+    hipLaunchKernelGGL((fir_poly_kernel<false, true, true>), dim3((unsigned)g_tune_fir_grid), blk, 0, st, x,
+                       n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+#endif
   else if (x4_aligned(x, g0 - lo2, hop))
     hipLaunchKernelGGL((fir_poly_kernel<false, true>), g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw,
                        twd, m);

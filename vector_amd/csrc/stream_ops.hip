@@ -177,6 +177,8 @@ hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* 
 
 #ifdef VSIG_TUNING
 namespace vsig {
+int g_tune_fir_grid = 0, g_tune_xcorr_grid = 0;
+
 // ---------------------------------------------------------------- copy probe
 // HBM ceiling probe for the tuning tools (tools/membw.py): copy n complex64
 // with 8-B (float2) or 16-B (float4) lanes, plain or non-temporal stores.

@@ -543,6 +543,12 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else if (k == "refine_cap") {
     if (value < 4096) return fail(c, VSIG_E_INVALID, "refine_cap must be >= 4096");
     c->refine_cap = value;
+#ifdef VSIG_TUNING
+  } else if (k == "tune_fir_grid") {
+    vsig::g_tune_fir_grid = value > 0 ? value : 0;
+  } else if (k == "tune_xcorr_grid") {
+    vsig::g_tune_xcorr_grid = value > 0 ? value : 0;
+#endif
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }

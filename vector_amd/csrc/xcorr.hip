@@ -348,7 +348,7 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
   wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
 }
 
-template <class P>
+template <class P, bool PERSIST = false>
 __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
@@ -359,11 +359,20 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   static_assert(P::TF % (M / 64) == 0 && (P::N / P::R[0]) % (M / 64) == 0,
                 "per-element split twiddles must be 64th roots of unity");
   __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
-  const int t = threadIdx.x;
-  const long long b = xcd_remap(blockIdx.x, gridDim.x);
-  if (b >= nblocks) return;
+  const int t0 = threadIdx.x;
   float2 wa[nanch_total<P>()];
-  load_anchors<P>(wa, tw, t);
+  load_anchors<P>(wa, tw, t0);
+  // PERSIST (tuning builds): a fixed grid walks the blocks (grid-stride)
+  for (long long it = PERSIST ? blockIdx.x : 0;; it += gridDim.x) {
+  const long long b = PERSIST ? it : xcd_remap(blockIdx.x, gridDim.x);
+  if (b >= nblocks) return;
+  if constexpr (PERSIST) __syncthreads();        // the previous block's LDS reads
+  // per-iteration thread index and tables opaque to LICM (else every
+  // iteration's addresses and table loads are hoisted and pinned in VGPRs)
+  const int zz = PERSIST ? opaque_zero() : 0;
+  const int t = t0 + zz;
+  const float4* __restrict__ Psz = Ps2 + zz;
+  const float2* __restrict__ wtz = wt + zz;
   auto fft2 = [&](float2* x, float2* y) {
     launder_anchors<P>(wa);
     fft_pair<P>(x, y, lds, TwAnchors{wa}, t);
@@ -371,8 +380,8 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   float2 a[P::E], d[P::E];
   load_halves<P>(a, d, s, b * hop - off, n, t, x4);
   // W_M^base: base = in_index(t, 0) (and in_index(t, R0) for the interleaved map)
-  const float2 w = wt[in_index<P>(t, 0)];
-  const float2 w1 = plan_ilv<P>() ? wt[in_index<P>(t, P::R[0])] : w;
+  const float2 w = wtz[in_index<P>(t, 0)];
+  const float2 w1 = plan_ilv<P>() ? wtz[in_index<P>(t, P::R[0])] : w;
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 x0 = a[e], x1 = d[e];
@@ -382,7 +391,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   fft2(a, d);
 #ifndef VSIG_NO_BUFLD
   if constexpr (!plan_ilv<P>()) {
-    const auto rp = make_rsrc(Ps2, (unsigned)P::N * (unsigned)sizeof(float4));
+    const auto rp = make_rsrc(Psz, (unsigned)P::N * (unsigned)sizeof(float4));
     const unsigned v0 = (unsigned)out_index<P>(t, 0) * (unsigned)sizeof(float4);
     static_for<0, P::E>([&](auto ei) {
       constexpr int e = decltype(ei)::value;
@@ -395,7 +404,7 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
   {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
-      const float4 p = Ps2[out_index<P>(t, e)];
+      const float4 p = Psz[out_index<P>(t, e)];
       a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
       d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
     }
@@ -409,6 +418,8 @@ __global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel
     d[e] = csub(ev, o);
   });
   xcorr_half_epilogue<P>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
+  if constexpr (!PERSIST) return;
+  }
 }
 
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
@@ -421,6 +432,14 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (M == 16384) {
     // every segment start s - off + b hop 16-byte aligned: 16-byte loads
     const bool x4 = hop % 2 == 0 && ((reinterpret_cast<uintptr_t>(s) - 8 * (uintptr_t)off) & 15) == 0;
+#ifdef VSIG_TUNING
+    if (g_tune_xcorr_grid > 0) {
+      hipLaunchKernelGGL((xcorr_half_kernel<PlanX16k, true>), dim3((unsigned)g_tune_xcorr_grid),
+                         dim3(PlanX16k::TF), 0, st, s, n, reinterpret_cast<const float4*>(Ps), off, nout,
+                         hop, c, store_mode, partials, nblocks, tw, wt, x4, lkeys);
+      return hipGetLastError();
+    }
+#endif
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
                        partials, nblocks, tw, wt, x4, lkeys);
