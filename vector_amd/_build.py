@@ -17,7 +17,7 @@ CSRC = os.path.join(HERE, "csrc")
 LIB = os.path.join(HERE, "libvsig.so")
 SOURCES = ["psd.hip", "fir.hip", "xcorr.hip", "reduce.hip", "refine.hip", "bigfft.hip", "analysis.hip", "pfb.hip",
            "stream_ops.hip", "chain.hip", "vsig_api.hip"]
-HEADERS = ["fft_engine.hpp", "os_common.hpp", "vsig_kernels.h"]
+HEADERS = ["fft_engine.hpp", "os_common.hpp", "vsig_kernels.h", "npabs.hpp"]
 ARCH = os.environ.get("VSIG_ARCH", "gfx950")
 
 

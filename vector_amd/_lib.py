@@ -153,6 +153,20 @@ def load_library(path: str | None = None):
         return lib
 
 
+def numpy_blas_threads() -> int:
+    """The thread count of the OpenBLAS behind this process's numpy (its zdotu
+    splits a complex128 dot of more than 10000 terms into that many chunks,
+    which decides the rounding of np.correlate's long sums); 1 if unknown."""
+    try:
+        from threadpoolctl import threadpool_info
+        for d in threadpool_info():
+            if d.get("internal_api") == "openblas":
+                return max(1, min(1024, int(d.get("num_threads", 1))))
+    except Exception:
+        pass
+    return 1
+
+
 class Context:
     """One vsig_ctx on one device (the library's stream state lives here)."""
 
@@ -164,6 +178,9 @@ class Context:
             raise VsigUnavailable(f"vsig_init(device={device}) failed: "
                                   f"{lib.vsig_errstr(rc).decode()}")
         self.lib, self.h, self.device = lib, h, device
+        # the refine matches numpy's complex128 sums operation for operation;
+        # OpenBLAS splits those over 10000 terms across its threads
+        self.check(lib.vsig_set_option(h, b"blas_threads", numpy_blas_threads()), "blas_threads")
 
     def check(self, rc: int, what: str):
         if rc != VSIG_OK:

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include "vsig_kernels.h"
+#include "npabs.hpp"
 
 namespace vsig {
 
@@ -127,36 +128,15 @@ __global__ __launch_bounds__(256) void thresh_reduce(const T* __restrict__ a, lo
 // 256 x 16 elements: tile sums -> scan of tile sums (one block) -> tile prefix.
 constexpr int SCAN_T = 256, SCAN_E = 16, SCAN_TILE = SCAN_T * SCAN_E;
 
-// np.abs of a complex value as numpy's SIMD loop computes it
-// (loops_unary_complex): L * sqrt(fma(r, r, 1)), r = S / L with L / S the
-// larger / smaller of |re|, |im| — not the correctly rounded hypot.
-__device__ __forceinline__ float cabs_np(float re, float im) {
-  const float a = fabsf(re), b = fabsf(im);
-  const float L = fmaxf(a, b), S = fminf(a, b);
-  if (L == 0.f || isinf(L)) return L;
-  // float division / sqrt / product correctly rounded through double
-  // (53 >= 2*24 + 2: no double-rounding error)
-  const float r = (float)((double)S / (double)L);
-  const float q = (float)sqrt((double)fmaf(r, r, 1.f));
-  return (float)((double)L * (double)q);
-}
-__device__ __forceinline__ double cabs_np(double re, double im) {
-  const double a = fabs(re), b = fabs(im);
-  const double L = fmax(a, b), S = fmin(a, b);
-  if (L == 0.0 || isinf(L)) return L;
-  const double r = __ddiv_rn(S, L);
-  return __dmul_rn(L, __dsqrt_rn(fma(r, r, 1.0)));
-}
-
 // |x|^2 exactly as numpy forms np.abs(x) ** 2 (squared in the abs's dtype).
 __device__ __forceinline__ double energy_of(const float2* x, long long i) {
   const float2 v = x[i];
-  const float h = cabs_np(v.x, v.y);
+  const float h = np_cabs(v.x, v.y);
   return (double)__fmul_rn(h, h);
 }
 __device__ __forceinline__ double energy_of(const double2* x, long long i) {
   const double2 v = x[i];
-  const double h = cabs_np(v.x, v.y);
+  const double h = np_cabs(v.x, v.y);
   return __dmul_rn(h, h);
 }
 __device__ __forceinline__ double energy_of(const float* x, long long i) {
@@ -269,9 +249,9 @@ __global__ __launch_bounds__(256) void db_transform_f32(const float* __restrict_
     out[i] = __fmul_rn(10.f, (float)log10((double)__fadd_rn(fabsf(a[i]), floor_)));
 }
 
-// |a| + 0j (np.abs as numpy computes it: complex -> cabs_np, real -> fabs),
+// |a| + 0j (np.abs as numpy computes it: complex -> np_cabs, real -> fabs),
 // written as complex64 (O = float2) or complex128 (O = double2).
-template <class T> __device__ __forceinline__ double absd(const T& v) { return cabs_np(v.x, v.y); }
+template <class T> __device__ __forceinline__ double absd(const T& v) { return np_cabs(v.x, v.y); }
 template <> __device__ __forceinline__ double absd<double>(const double& v) { return fabs(v); }
 template <> __device__ __forceinline__ double absd<float>(const float& v) { return (double)fabsf(v); }
 template <class O> __device__ __forceinline__ O mk_re(double r);

@@ -5,8 +5,10 @@
 #pragma once
 #include "fft_engine.hpp"
 #include "vsig_kernels.h"
+#include "npabs.hpp"
 
 namespace vsig {
+
 
 // Streaming accesses (input read once, output written once) with a
 // non-temporal hint where it measured faster on the chain: the PSD's frame

@@ -6,15 +6,16 @@ namespace vsig {
 
 // ---------------------------------------------------------------------------
 // |c| reduction over an array in double precision (find_correlation_peak,
-// utils.py:1321-1334): |c| = hypot(re, im) like np.abs, first max wins.
+// utils.py:1321-1334): |c| = numpy's own complex abs (np_cabs, in the array's
+// precision), first max wins.
 // T = double2 (complex128), float2 (complex64), double, float.
 // ---------------------------------------------------------------------------
 template <class T> __device__ __forceinline__ double absval(const T* p, long long i);
 template <> __device__ __forceinline__ double absval<double2>(const double2* p, long long i) {
-  const double2 v = p[i]; return hypot(v.x, v.y);
+  const double2 v = p[i]; return np_cabs(v.x, v.y);
 }
 template <> __device__ __forceinline__ double absval<float2>(const float2* p, long long i) {
-  const float2 v = p[i]; return (double)hypotf(v.x, v.y);
+  const float2 v = p[i]; return (double)np_cabs(v.x, v.y);
 }
 template <> __device__ __forceinline__ double absval<double>(const double* p, long long i) { return fabs(p[i]); }
 template <> __device__ __forceinline__ double absval<float>(const float* p, long long i) { return (double)fabsf(p[i]); }

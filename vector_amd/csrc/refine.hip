@@ -19,14 +19,23 @@
 //             (q / rsub), see xcorr.hip); for a stored c64 array, its
 //             64-output chunks holding one;
 //   stage 1 : every output of every item by a plain fp64 direct sum
-//             c[o] = sum_k a[i - (nv-1) + k] conj(v[k]), i = F + o (the same
-//             formula numpy evaluates), max |c|^2 by a 64-bit atomic max;
-//   stage 2 : outputs within eps2 of the stage-1 max again by a compensated
-//             dot product (Ogita-Rump-Oishi Dot2: TwoProd by FMA + TwoSum,
-//             as accurate as a 2x-precision sum rounded once), then the max
-//             |c|^2 and the lowest output index attaining it (np.argmax's
-//             first-max rule) by the last stage-2 block, which replaces the
-//             peak record's max / index (sums untouched);
+//             c[o] = sum_k a[i - (nv-1) + k] conj(v[k]), i = F + o, with the
+//             sum S of the products' component magnitudes; that bounds how far
+//             both this sum and numpy's own (below) lie from the exact value:
+//             |c| +- E, E = (n/8 + n/64 + T + 300) 2^-52 S + 2^-49 |c|; the
+//             largest lower end (|c| - E) by a 64-bit atomic max;
+//   stage 2 : the outputs whose upper end reaches that lower end, evaluated in
+//             numpy's own operation order -- np.correlate's complex128 dot is
+//             OpenBLAS zdotu (8 fma accumulators per component over complex
+//             k mod 8, a fixed add tree, a scalar fma tail, re = d0 - d1,
+//             im = d2 + d3; above 10000 terms split over T = blas_threads
+//             chunks added in order), |c| by numpy's complex abs (larger *
+//             sqrt(fma(r, r, 1)), r = smaller / larger) -- so every value is
+//             numpy's to the bit (oracle/npdot.c restates it on the CPU and
+//             tests/test_npdot_cpu.py pins it against numpy).  np.argmax's
+//             rule then applies as is: the max |c| and the lowest output index
+//             attaining it, by the last stage-2 block, which replaces the peak
+//             record's max / index (sums untouched);
 //   patch   : optionally the refined values into a complex128 c.
 // All sizes on the device (no host synchronisation); more than `cap` items
 // leaves the record as the fp32 pass produced it and sets status = 1.
@@ -37,20 +46,6 @@
 namespace vsig {
 
 #pragma clang fp contract(off)
-
-__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
-  s = a + b;
-  const double bb = s - a;
-  e = (a - (s - bb)) + (b - bb);
-}
-__device__ __forceinline__ void dot2_add(double& s, double& c, double x, double y) {
-  const double p = x * y;
-  const double pe = __builtin_fma(x, y, -p);
-  double t, te;
-  two_sum(s, p, t, te);
-  s = t;
-  c += te + pe;
-}
 
 template <class T> __device__ __forceinline__ double2 ld2(const T* p, long long i);
 template <> __device__ __forceinline__ double2 ld2<float2>(const float2* p, long long i) {
@@ -244,6 +239,8 @@ struct RefineGeom {
   int wstep, rsub;      //   wave base step, 64-output rows per stride step
   int cols;             // > 0: items are thread columns (wave p, column l) =
                         //   p * 64 + l, cols rows each (xcorr_lane_keys)
+  int nthr;             // OpenBLAS threads of the numpy being matched (zdotu
+                        //   splits sums over 10000 terms into nthr chunks)
 };
 
 __device__ __forceinline__ long long item_output(const RefineGeom& g, long long item, int q, int l) {
@@ -281,9 +278,9 @@ __device__ __forceinline__ long long unit_output(const RefineGeom& g, long long 
 template <class T>
 __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __restrict__ v,
                                            long long abase, long long k0, long long k1,
-                                           double& re, double& im) {
+                                           double& re, double& im, double& sa) {
   long long k = k0;
-  double r0 = 0, r1 = 0, i0 = 0, i1 = 0;
+  double r0 = 0, r1 = 0, i0 = 0, i1 = 0, s0 = 0, s1 = 0;
   for (; k + 8 <= k1; k += 8) {
     double2 x[8], y[8];
 #pragma unroll
@@ -292,17 +289,29 @@ __device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __r
     for (int j = 0; j < 8; j += 2) {
       r0 = fma(x[j].x, y[j].x, r0); r0 = fma(x[j].y, y[j].y, r0);
       i0 = fma(x[j].y, y[j].x, i0); i0 = fma(-x[j].x, y[j].y, i0);
+      s0 = fma(fabs(x[j].x) + fabs(x[j].y), fabs(y[j].x) + fabs(y[j].y), s0);
       r1 = fma(x[j + 1].x, y[j + 1].x, r1); r1 = fma(x[j + 1].y, y[j + 1].y, r1);
       i1 = fma(x[j + 1].y, y[j + 1].x, i1); i1 = fma(-x[j + 1].x, y[j + 1].y, i1);
+      s1 = fma(fabs(x[j + 1].x) + fabs(x[j + 1].y), fabs(y[j + 1].x) + fabs(y[j + 1].y), s1);
     }
   }
   for (; k < k1; ++k) {
     const double2 x = ld2<T>(a, abase + k), y = ld2<T>(v, k);
     r0 = fma(x.x, y.x, r0); r0 = fma(x.y, y.y, r0);
     i0 = fma(x.y, y.x, i0); i0 = fma(-x.x, y.y, i0);
+    s0 = fma(fabs(x.x) + fabs(x.y), fabs(y.x) + fabs(y.y), s0);
   }
   re = r0 + r1;
   im = i0 + i1;
+  sa = s0 + s1;
+}
+
+// Half-width of the interval around a stage-1 |c| that holds both the exact
+// |c| and numpy's (see the header): n overlap terms, S the sum of the
+// products' component magnitudes (>= 1 ulp-scale error sources of both sums).
+__device__ __forceinline__ double np_band(long long n, int nthr, double S, double c1) {
+  const double m = (double)(n / 8 + n / 64 + nthr + 300);
+  return m * 0x1p-52 * S + 0x1p-49 * c1;
 }
 
 constexpr int kS1Waves = 16;
@@ -322,7 +331,7 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
   const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int ol = l & (OUTS - 1);                    // output within the block
   const int ch = w * (64 / OUTS) + (l / OUTS);      // tap chunk
-  __shared__ double pr[kChunks][OUTS], pi[kChunks][OUTS];
+  __shared__ double pr[kChunks][OUTS], pi[kChunks][OUTS], pa[kChunks][OUTS];
   for (long long ub = blockIdx.x; ub < nunits * kSplit; ub += gridDim.x) {   // uniform per block
     const long long u = ub / kSplit;
     const int sub = (int)(ub - u * kSplit);
@@ -330,30 +339,39 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
     const int q = (int)(u % g.Q);
     const int po = sub * OUTS + ol;                 // output's place in the unit (0..63)
     const long long o = unit_output(g, item, q, po);
-    double re = 0.0, im = 0.0;
+    double re = 0.0, im = 0.0, sa = 0.0;
+    long long k0 = 0, k1 = 0;
     if (o >= 0) {
       const long long i = g.F + o;
-      long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
       const long long span = (k1 - k0 + kChunks - 1) / kChunks;      // this chunk's share
       const long long q0 = k0 + ch * span;
       const long long q1 = q0 + span < k1 ? q0 + span : k1;
-      if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im);
+      if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im, sa);
     }
     pr[ch][ol] = re;
     pi[ch][ol] = im;
+    pa[ch][ol] = sa;
     __syncthreads();
-    if (threadIdx.x < OUTS) {                       // lanes 0..OUTS-1 of wave 0: output ol
+    if (threadIdx.x < OUTS) {                       // lanes 0..OUTS-1 of wave 0 (chunk 0): output ol
       re = 0.0;
       im = 0.0;
+      sa = 0.0;
 #pragma unroll 8
-      for (int c = 0; c < kChunks; ++c) { re += pr[c][ol]; im += pi[c][ol]; }
-      const double m2 = o >= 0 ? re * re + im * im : -1.0;
+      for (int c = 0; c < kChunks; ++c) { re += pr[c][ol]; im += pi[c][ol]; sa += pa[c][ol]; }
+      // vals: the upper end of the output's interval, max1: the largest lower end
+      double up = -1.0, lo = -1.0;
+      if (o >= 0) {
+        const double c1 = sqrt(re * re + im * im);
+        const double E = np_band(k1 - k0, g.nthr, sa, c1);
+        up = c1 + E;
+        lo = c1 - E > 0.0 ? c1 - E : 0.0;
+      }
       const long long e = u * 64 + po;
-      vals[e] = m2;
+      vals[e] = up;
       oidx[e] = o;
       cv[e] = make_double2(re, im);
-      double wm = m2;
+      double wm = lo;
 #pragma unroll
       for (int off = OUTS / 2; off > 0; off >>= 1) {
         const double o2 = __shfl_xor(wm, off);
@@ -365,26 +383,82 @@ __global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restri
   }
 }
 
-// Stage 2: the outputs within eps2 of the stage-1 max recomputed by a
-// compensated dot product, one 1024-thread block per output (thread i takes
-// taps k = i mod 1024, four loads in flight: one batch for a 4096-tap
-// template; Dot2 partials (s, c) per thread, combined across lanes and then
-// across the 16 waves in wave order by TwoSum, which keeps Dot2's bound); the
-// others drop out (vals = -1).  The last block to finish takes the argmin
-// (the lowest output index attaining the max |c|^2, np.argmax's rule) and
-// writes the record (one launch instead of stage 2 + argmin + finish).
-__device__ __forceinline__ void two_sum_pair(double& s, double& c, double s2, double c2) {
-  double t, e;
-  two_sum(s, s2, t, e);
-  s = t;
-  c = c + c2 + e;
-}
-
+// Stage 2: numpy's value of every output whose interval reaches the largest
+// lower end (see the header), then np.argmax.  One 8-lane group per output
+// (a wave takes up to 8 outputs): lane s of the group runs OpenBLAS zdot
+// kernel slot s -- the four fma chains over complex k = s mod 8 of the block
+// part n8 = n & -8 of a chunk -- the add tree combines the slots exactly as
+// zdot_kernel_8 does ((s, s^2), then (s, s^4), then the two 128-bit halves:
+// s, s^1), and slot 0 runs the scalar tail.  Chunks (OpenBLAS threads, only
+// above 10000 terms) run one after another in the group and are added in
+// order onto zero, as zdotu_k does.  Every step is an IEEE double fma / add /
+// sub / div / sqrt, so the values are numpy's bit for bit.
 constexpr int kS2Threads = 1024;
+constexpr long long kBlasThreadMin = 10000;   // zdotu_k: threads only above this n
+
+template <class T>
+__device__ __forceinline__ double2 ldc(const T* p, long long i) { return ld2<T>(p, i); }
+
+// One zdot_compute over chunk [c0, c0 + w) of the overlap (x = a + ax, y =
+// conj(v)); the result in slot 0 (lane s == 0) of the group.
+template <class T>
+__device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* __restrict__ v,
+                                              long long ax, long long c0, long long w, int s,
+                                              double& re, double& im) {
+  const long long n8 = w & ~7LL;
+  double P = 0.0, Q = 0.0, R = 0.0, U = 0.0;     // xr yr, xi yi, xr yi, xi yr
+  long long k = s;
+  for (; k + 56 < n8; k += 64) {                  // 8 rows in flight
+    double2 x[8], y[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x[j] = ldc<T>(a, ax + c0 + k + 8 * j);
+      y[j] = ldc<T>(v, c0 + k + 8 * j);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const double yi = -y[j].y;
+      P = fma(x[j].x, y[j].x, P);
+      Q = fma(x[j].y, yi, Q);
+      R = fma(x[j].x, yi, R);
+      U = fma(x[j].y, y[j].x, U);
+    }
+  }
+  for (; k < n8; k += 8) {
+    const double2 x = ldc<T>(a, ax + c0 + k), y = ldc<T>(v, c0 + k);
+    const double yi = -y.y;
+    P = fma(x.x, y.x, P);
+    Q = fma(x.y, yi, Q);
+    R = fma(x.x, yi, R);
+    U = fma(x.y, y.x, U);
+  }
+  // (A0 + A1) + (A2 + A3) per ymm lane, then low + high halves
+  P = P + __shfl_xor(P, 2, 8);  Q = Q + __shfl_xor(Q, 2, 8);
+  R = R + __shfl_xor(R, 2, 8);  U = U + __shfl_xor(U, 2, 8);
+  P = P + __shfl_xor(P, 4, 8);  Q = Q + __shfl_xor(Q, 4, 8);
+  R = R + __shfl_xor(R, 4, 8);  U = U + __shfl_xor(U, 4, 8);
+  double d0 = P + __shfl_xor(P, 1, 8), d1 = Q + __shfl_xor(Q, 1, 8);
+  double d2 = R + __shfl_xor(R, 1, 8), d3 = U + __shfl_xor(U, 1, 8);
+  if (s == 0) {
+    for (long long t = n8; t < w; ++t) {
+      const double2 x = ldc<T>(a, ax + c0 + t), y = ldc<T>(v, c0 + t);
+      const double yi = -y.y;
+      d0 = fma(x.x, y.x, d0);
+      d1 = fma(x.y, yi, d1);
+      d2 = fma(x.x, yi, d2);
+      d3 = fma(y.x, x.y, d3);
+    }
+  }
+  double r = d0 - d1;
+  const double m = d2 + d3;
+  r = fma(m, 0.0, r);
+  re = r;
+  im = m;
+}
 
 template <class T>
 __global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict__ a, const T* __restrict__ v,
-                                                            RefineGeom g, long long cap, double eps2,
+                                                            RefineGeom g, long long cap,
                                                             RefineKeys* __restrict__ keys,
                                                             double* __restrict__ vals,
                                                             const long long* __restrict__ oidx,
@@ -395,18 +469,17 @@ __global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict_
   const long long cnt = (long long)keys->count;
   if (keys->status || cnt == 0) return;            // uniform: no block counts itself
   const long long n = (cnt < cap ? cnt : cap) * g.Q * 64;
-  const double m1 = __longlong_as_double((long long)keys->max1);
-  const double thr = m1 * (1.0 - eps2);
+  const double lo1 = __longlong_as_double((long long)keys->max1);
   const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
+  const int grp = l >> 3, s = l & 7;
   __shared__ unsigned long long smask;
-  __shared__ double ps[NW][4];
   __shared__ int slast;
   __shared__ long long smin;
   for (long long base = (long long)blockIdx.x * 64; base < n; base += (long long)gridDim.x * 64) {
     if (w == 0) {                                  // 64 entries per block step
       const long long e = base + l;
       const double v1 = e < n ? vals[e] : -1.0;
-      const bool surv = v1 >= 0.0 && v1 >= thr;
+      const bool surv = v1 >= 0.0 && v1 >= lo1;
       if (e < n && v1 >= 0.0 && !surv) vals[e] = -1.0;
       const unsigned long long m = __ballot(surv);
       if (l == 0) smask = m;
@@ -418,61 +491,45 @@ __global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict_
       if (surv && (long long)j < cap) items[j] = e;
     }
     __syncthreads();
-    unsigned long long mask = smask;
-    while (mask) {                                 // uniform
-      const int src = __builtin_ctzll(mask);
-      mask &= mask - 1;
+    // survivors in mask order, in batches of 8: batch b -> wave b % NW, its
+    // r-th survivor -> group r (the groups of a wave run side by side)
+    const unsigned long long mask = smask;
+    const int nsv = __popcll(mask);
+    for (int b = w; b * 8 < nsv; b += NW) {        // uniform per wave
+      const int r = b * 8 + grp;
+      if (r >= nsv) continue;                      // uniform per group
+      unsigned long long mm = mask;
+      for (int q = 0; q < r; ++q) mm &= mm - 1;
+      const int src = __builtin_ctzll(mm);
       const long long es = base + src;
       const long long i = g.F + oidx[es];
       long long k0, k1;
       tap_range(i, g.na, g.nv, k0, k1);
-      const long long abase = i - (g.nv - 1);
-      double sr = 0.0, cr = 0.0, si = 0.0, ci = 0.0;
-      long long k = k0 + tid;
-      for (; k + 3 * kS2Threads < k1; k += 4 * kS2Threads) {
-        double2 x[4], y[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          x[j] = ld2<T>(a, abase + k + kS2Threads * j);
-          y[j] = ld2<T>(v, k + kS2Threads * j);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          dot2_add(sr, cr, x[j].x, y[j].x);
-          dot2_add(sr, cr, x[j].y, y[j].y);
-          dot2_add(si, ci, x[j].y, y[j].x);
-          dot2_add(si, ci, -x[j].x, y[j].y);
-        }
+      const long long nt = k1 - k0;
+      const long long ax = i - (g.nv - 1);
+      const int nch = (nt <= kBlasThreadMin || g.nthr <= 1) ? 1 : g.nthr;
+      double re = 0.0, im = 0.0;
+      long long rest = nt, c0 = k0;
+      for (int t = 0; t < nch && rest > 0; ++t) {
+        long long wd = (rest + (nch - t) - 1) / (nch - t);
+        if (wd > rest) wd = rest;
+        double pr, pi;
+        np_zdot_chunk<T>(a, v, ax, c0, wd, s, pr, pi);
+        re = re + pr;
+        im = im + pi;
+        c0 += wd;
+        rest -= wd;
       }
-      for (; k < k1; k += kS2Threads) {
-        const double2 x = ld2<T>(a, abase + k);
-        const double2 y = ld2<T>(v, k);
-        dot2_add(sr, cr, x.x, y.x);
-        dot2_add(sr, cr, x.y, y.y);
-        dot2_add(si, ci, x.y, y.x);
-        dot2_add(si, ci, -x.x, y.y);
-      }
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        two_sum_pair(sr, cr, __shfl_xor(sr, off), __shfl_xor(cr, off));
-        two_sum_pair(si, ci, __shfl_xor(si, off), __shfl_xor(ci, off));
-      }
-      if (l == 0) { ps[w][0] = sr; ps[w][1] = cr; ps[w][2] = si; ps[w][3] = ci; }
-      __syncthreads();
-      if (tid == 0) {
-        sr = ps[0][0]; cr = ps[0][1]; si = ps[0][2]; ci = ps[0][3];
-        for (int q = 1; q < NW; ++q) {
-          two_sum_pair(sr, cr, ps[q][0], ps[q][1]);
-          two_sum_pair(si, ci, ps[q][2], ps[q][3]);
-        }
-        const double re = sr + cr, im = si + ci;
-        const double m2 = re * re + im * im;
-        vals[es] = m2;
+      if (s == 0) {
+        re = 0.0 + re;                             // numpy's CDOUBLE_dot sum
+        im = 0.0 + im;
+        const double av = np_cabs(re, im);
+        vals[es] = av;
         cv[es] = make_double2(re, im);
-        atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(m2));
+        atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(av));
       }
-      __syncthreads();
     }
+    __syncthreads();
   }
   // the last block to finish: argmin over the entries, then the record (one
   // release per block: the block's stores are complete at the barrier above)
@@ -508,7 +565,7 @@ __global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict_
   if (l == 0) atomicMin(&smin, mi);
   __syncthreads();
   if (tid == 0 && smin != 0x7fffffffffffffffLL) {
-    rec->max2 = sqrt(m2);
+    rec->max2 = m2;                                // numpy's |c| at its argmax
     rec->idx = smin;
   }
 }
@@ -545,7 +602,7 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   long long* oidx = reinterpret_cast<long long*>(vals + n);
   double2* cv = reinterpret_cast<double2*>(oidx + n);
   RefineGeom g{r.nout, r.F, r.na, r.nv, r.rev, r.from_array, r.hop, r.waves, r.Q, r.stride,
-               r.wstep, r.rsub, r.cols};
+               r.wstep, r.rsub, r.cols, r.blas_threads > 1 ? r.blas_threads : 1};
   PeakPartial* rec = r.rec;
   if (r.finalize) {              // the partials' finalize + select in one launch
     if (r.from_array || !r.tmp || !r.done) return hipErrorInvalidValue;
@@ -595,7 +652,7 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
       hipLaunchKernelGGL((refine_stage1<T, 16>), dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
                          r.cap_items, keys, vals, oidx, cv);
     hipLaunchKernelGGL(refine_stage2<T>, dim3(g2), dim3(kS2Threads), 0, st, a, v, g, r.cap_items,
-                       r.eps2, keys, vals, oidx, cv, rec, items);
+                       keys, vals, oidx, cv, rec, items);
   };
   if (r.c128) stages(double2{});
   else stages(float2{});

@@ -36,6 +36,7 @@ struct vsig_ctx {
   int refine = 1;                        // exact re-rank of the correlators' peak
   int refine_eps_ppm = 1000;             // fp32 candidate band (relative, ppm of max |c|)
   long long refine_cap = 1LL << 20;      // max outputs revisited (else record left fp32)
+  int blas_threads = 1;                  // numpy's OpenBLAS threads (its zdotu splits > 10000 terms)
   bool refine_ran = false;
   struct Chirp { long long M; float2* c; float2* B; };
   std::map<long long, Chirp> chirps;     // Bluestein plans by length (bigfft.hip)
@@ -302,7 +303,7 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
     }
   }
   r.eps = c->refine_eps_ppm * 1e-6;
-  r.eps2 = 1e-6;
+  r.blas_threads = c->blas_threads;
   r.cap_items = c->refine_cap / (64LL * r.Q);
   if (r.cap_items < 1) r.cap_items = 1;
   int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, vsig::refine_scratch_bytes(r.cap_items, r.Q));
@@ -543,6 +544,9 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else if (k == "refine_cap") {
     if (value < 4096) return fail(c, VSIG_E_INVALID, "refine_cap must be >= 4096");
     c->refine_cap = value;
+  } else if (k == "blas_threads") {
+    if (value < 1 || value > 1024) return fail(c, VSIG_E_INVALID, "blas_threads must be in [1, 1024]");
+    c->blas_threads = value;
 #ifdef VSIG_TUNING
   } else if (k == "tune_fir_grid") {
     vsig::g_tune_fir_grid = value > 0 ? value : 0;
@@ -561,6 +565,7 @@ int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
   if (k == "refine") *value = c->refine;
   else if (k == "refine_eps_ppm") *value = c->refine_eps_ppm;
   else if (k == "refine_cap") *value = (int)c->refine_cap;
+  else if (k == "blas_threads") *value = c->blas_threads;
   else return VSIG_E_INVALID;
   return VSIG_OK;
 }

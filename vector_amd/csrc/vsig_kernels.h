@@ -158,7 +158,8 @@ struct RefineArgs {
   long long nparts, hop;
   int waves, Q, stride;             // wave w of block b: ob + wstep w + l + 64 (q % rsub)
   int wstep, rsub;                  //   + stride (q / rsub), l < 64, q < Q (xcorr_geom)
-  double eps, eps2;                 // fp32 band, stage-2 band (relative)
+  double eps;                       // fp32 candidate band (relative)
+  int blas_threads;                 // OpenBLAS threads of the numpy matched (sums > 10000)
   int cols;                         // > 0: thread-column items from lane keys (Q = 1;
   const unsigned* lkeys;            //   cols rows each), lkeys: 64 per wave partial
   int finalize;                     // finalize the partials here (+ select, one launch):
