@@ -10,7 +10,7 @@ FIR, decimate by 4, 8192-point Hann PSD (hop 8192) of the decimated stream,
 contiguous samples each (strong scaling), exchanging only the FIR / correlation
 halos and 32-byte peak records over RCCL.
 
-  python bench.py [--gpus N --steps K --warmup W]
+  python bench.py [--gpus N --steps K --warmup W]   # N > 1: starts its N ranks itself
   python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
   python bench.py --workload c2       # configs[1]: 2**28 samples / GPU, D = 1 (+ the sync
                                       #   stage), north_star's FIR+FFT >= 70 % HBM target
@@ -168,6 +168,58 @@ WORKLOADS = {
 }
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without a launcher: start N child processes of this
+    script (one per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
+    127.0.0.1) -- before anything here touches the GPU, and as children, never
+    by exec.  Rank 0's stdout carries the one JSON line.  Returns the first
+    non-zero child exit code (the others are stopped then), else 0."""
+    import subprocess
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code if code > 0 else 1
+                log(f"bench: rank {procs.index(p)} exited with {code}; stopping the others")
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def _launcher_selftest(args, world, rank, local):
+    """Rendezvous over gloo (CPU only) and report what each rank was given
+    (tests/test_bench_launch.py)."""
+    dist.init_process_group("gloo")
+    info = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
+                                           "MASTER_PORT")}
+    json.dump(info, open(os.path.join(args.launcher_selftest, f"rank{rank}.json"), "w"))
+    t = torch.tensor([rank + 1.0])
+    dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "n_gpus": world, "rccl_world": dist.get_world_size(),
+                          "sum_ranks": float(t.item())}), flush=True)
+    dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -202,14 +254,18 @@ def main():
                     help="FIR / PSD / xcorr on their own HIP streams (default: one stream)")
     ap.add_argument("--nchan", type=int, default=64)
     ap.add_argument("--branch-taps", type=int, default=16)
+    ap.add_argument("--launcher-selftest", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        raise SystemExit(launch_ranks(args.gpus, sys.argv[1:]))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with "
-                         "python -m torch.distributed.run --nproc-per-node N bench.py --gpus N")
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.launcher_selftest:
+        return _launcher_selftest(args, world, rank, local)
     torch.cuda.set_device(local)
     dev = torch.device(f"cuda:{local}")
     if world > 1:
@@ -393,6 +449,7 @@ def main():
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "stages_roofline": stage_roof,
         "check": check,
+        "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
     }
     print(json.dumps(out), flush=True)
     if world > 1:
@@ -579,6 +636,7 @@ def run_pfb(args, world, rank, local, dev):
                    "parallelism": f"time-chunk x{world} (RCCL right halo {P * nchan - nchan})"},
         "roofline": roof, "cpu_baseline": cpu,
         "check": {"frame1_rel_err": err, "ok": err < 1e-5},
+        "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
     }
     print(json.dumps(out), flush=True)
     if world > 1:
