@@ -115,7 +115,8 @@ int vsig_timing_read(vsig_ctx* ctx, const char* kernel, double* total_ms, int64_
 int vsig_timing_reset(vsig_ctx* ctx);
 
 /* ---- spectrum: Sxx[f, k] = |sum_{i<nperseg} w[i] x[f*hop + i] e^{-2 pi j k i / nfft}|^2 * scale
- * nfft: power of two in [64, 2^28] (above 16384: four-step FFT per frame);
+ * nfft: any length >= nperseg up to 2^27 (powers of two in [64, 2^28]: in-LDS plans, above
+ *   16384 a four-step FFT per frame; other lengths: Bluestein per frame, bigfft.hip);
  * nframes = (n - nperseg) / hop + 1;
  * sxx is frame-major float32 [nframes][nfft] (Sxx of scipy is its transpose);
  * shift = 1 stores bin k at (k + nfft/2) % nfft (np.fft.fftshift).
@@ -130,7 +131,9 @@ int vsig_psd_c64(vsig_ctx* ctx, const void* x, int64_t n, const float* win, int3
 
 /* ---- FIR: y[g] = sum_{m<ntaps} h[m] x[g*decim - m] (x = 0 outside [0, n)),
  * g in [0, ceil(n/decim)).  Taps complex64 on the host (real taps: imag = 0);
- * ntaps in [1, 8192]. */
+ * any ntaps >= 1 (np.convolve's contract, utils.py:802,816): up to 8192 one
+ * overlap-save pass, beyond that 8192-tap parts run undecimated and summed with
+ * their delays (a scratch of n samples). */
 int vsig_fir_create(vsig_ctx* ctx, const void* taps, int32_t ntaps, int32_t decim, vsig_fir** out);
 void vsig_fir_free(vsig_fir* fir);
 /* Overlap-save block size M chosen for the taps (0 for a null handle). */

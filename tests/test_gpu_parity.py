@@ -77,6 +77,22 @@ def test_spectrum_all_sizes_vs_oracle(gpu, nfft):
     assert_spectra_close(S, R)
 
 
+@pytest.mark.parametrize("nfft,nps,nov", [(100, 100, 0), (1000, 900, 300), (3000, 2500, 1250),
+                                          (48, 40, 20), (12_000, 12_000, 6000), (20_001, 9000, 0)])
+def test_spectrum_any_nfft_vs_oracle(gpu, nfft, nps, nov):
+    """scipy.signal.spectrogram takes any nfft >= nperseg (utils.py:281-291):
+    lengths that are not powers of two run as a Bluestein transform per frame
+    (in LDS up to 2 nfft - 1 <= 16384, four-step beyond)."""
+    x = ref.synth_iq(nfft * 6 + 333, seed=nfft)
+    f, t, S = gpu.spectrum(x, 3.0, "hann", nps, nov, nfft)
+    fr, tr, R = ref.spectrum(x, 3.0, "hann", nps, nov, nfft)
+    np.testing.assert_array_equal(f, fr)
+    np.testing.assert_array_equal(t, tr)
+    assert_spectra_close(S, R)
+    _, _, Ss = gpu.spectrum(x, 3.0, "hann", nps, nov, nfft, fftshift=True)
+    assert_spectra_close(Ss, np.fft.fftshift(R, axes=0))
+
+
 def test_spectrum_window_array_and_shift(gpu):
     x = ref.synth_iq(50_000, seed=9)
     w = np.kaiser(700, 5.0)
@@ -109,8 +125,6 @@ def test_spectrum_edge_cases(gpu):
         gpu.spectrum(x, 1.0, "hann", 256, 0, 128)              # nfft < nperseg
     with pytest.raises(ValueError):
         gpu.spectrum(x, 1.0, "hann", 256, 256, 256)            # noverlap >= nperseg
-    with pytest.raises(NotImplementedError):
-        gpu.spectrum(x, 1.0, "hann", 100, 0, 100)              # nfft not a power of two
     f, t, S = gpu.spectrum(np.zeros(0, np.complex64), 1.0)
     assert S.size == 0
 
@@ -164,8 +178,17 @@ def test_filter_complex_taps_and_short_input(gpu):
         assert_normwise(gpu.filter(x, taps, 1), ref.fir_filter(x, taps, 1), FIR_TOL)
     with pytest.raises(ValueError):
         gpu.filter(np.zeros(0, np.complex64), taps)
-    with pytest.raises(NotImplementedError):
-        gpu.filter(ref.synth_iq(100), np.ones(9000))
+
+
+@pytest.mark.parametrize("ntaps,n,decim", [(9000, 30_000, 1), (20_000, 50_000, 4), (16_384, 20_000, 3),
+                                           (9000, 100, 1)])
+def test_filter_long_taps_vs_oracle(gpu, ntaps, n, decim):
+    """np.convolve (utils.py:802, 816) has no length limit: filters over 8192
+    taps run as 8192-tap parts summed with their delays."""
+    rng = np.random.default_rng(ntaps + n)
+    x = ref.synth_iq(n, seed=n)
+    taps = (rng.standard_normal(ntaps) / np.sqrt(ntaps)).astype(np.float32)
+    assert_normwise(gpu.filter(x, taps, decim), ref.fir_filter(x, taps, decim), FIR_TOL)
 
 
 def test_filter_real_input_real_output(gpu):

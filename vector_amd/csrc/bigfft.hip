@@ -62,16 +62,24 @@ struct BfIn {                 // operand n of frame f of a forward pass
 
 struct BfOut {                // natural-order result n of frame f
   void* dst;
-  int kind;                   // 0 complex64, 1 complex128, 2 float64 real part, 3 complex64 real part
+  int kind;                   // 0 complex64, 1 complex128, 2 float64 real part, 3 complex64 real part,
+                              // 4 float32 |X|^2 * scale (PSD frames, optionally fftshift-ed)
   long long fstride;
   long long nout;             // store n < nout
   const float2* chirp;        // optional * chirp[n] (after conj)
   int conj;
   float scale;
+  int shift;
   __device__ __forceinline__ void operator()(long long f, long long n, float2 v) const {
     if (n >= nout) return;
     if (chirp) v = cmul(v, chirp[n]);        // c[k] S[k], then conj (inverse DFT)
     if (conj) v = cconj(v);
+    if (kind == 4) {                         // np.fft.fftshift: bin n at (n + nout // 2) % nout
+      long long o = n;
+      if (shift) { o = n + nout / 2; if (o >= nout) o -= nout; }
+      static_cast<float*>(dst)[f * fstride + o] = (v.x * v.x + v.y * v.y) * scale;
+      return;
+    }
     v = make_float2(v.x * scale, v.y * scale);
     const long long i = f * fstride + n;
     switch (kind) {
@@ -475,7 +483,7 @@ hipError_t launch_bf_icol(int N1, int N2, long long batch, float2* tmp, const Bi
                           const float2* tw1, const float2* t2, int S, int hiA, hipStream_t st) {
   const long long M = (long long)N1 * N2;
   BfIn bi{};
-  BfOut bo{out.dst, out.kind, out.fstride, out.nout, out.chirp, out.conj, out.scale};
+  BfOut bo{out.dst, out.kind, out.fstride, out.nout, out.chirp, out.conj, out.scale, out.shift};
   hipError_t e = col_dispatch(N1, [&](auto plan) {
     using PL = decltype(plan);
     constexpr int F = col_frames<PL>();
@@ -505,7 +513,7 @@ hipError_t launch_bf_row(int mode, int N1, int N2, long long batch, float2* tmp,
 hipError_t launch_bf_small(int mode, int M, long long batch, const BigIn& in, const BigOut& out,
                            const float2* Bk, const float2* tw, hipStream_t st) {
   BfIn bi{in.src, in.kind, in.fstride, in.estride, in.nvalid, in.chirp, in.win, in.conj, in.scale};
-  BfOut bo{out.dst, out.kind, out.fstride, out.nout, out.chirp, out.conj, out.scale};
+  BfOut bo{out.dst, out.kind, out.fstride, out.nout, out.chirp, out.conj, out.scale, out.shift};
   hipError_t e = plan_dispatch(M, [&](auto plan) {
     using PL = decltype(plan);
     if (mode == 0)

@@ -77,6 +77,27 @@ __global__ __launch_bounds__(256) void scale_c64(const float2* __restrict__ x, l
   }
 }
 
+// ------------------------------------------------ long FIR: delayed partial sums
+// A filter of more than 8192 taps runs as parts h_j = h[8192 j, 8192 (j+1)),
+// each an undecimated overlap-save FIR z_j = conv(x, h_j) over the whole
+// buffer; y[k] (+)= z_j[off + k D] with off = nhist - 8192 j (zero where the
+// index is negative: the delay reaches before the buffer).
+__global__ __launch_bounds__(256) void fir_part_accum(const float2* __restrict__ z, long long nz,
+                                                      long long off, int D, long long ny, int first,
+                                                      float2* __restrict__ y) {
+  const long long stride = (long long)gridDim.x * 256;
+  for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < ny; k += stride) {
+    const long long i = off + k * D;
+    const float2 v = (i >= 0 && i < nz) ? z[i] : make_float2(0.f, 0.f);
+    if (first) {
+      y[k] = v;
+    } else {
+      const float2 a = y[k];
+      y[k] = make_float2(a.x + v.x, a.y + v.y);
+    }
+  }
+}
+
 // ---------------------------------------------------------------- SMU-WV
 // numpy's float32 -> int16 cast on x86: truncate to int32 (out of range and
 // NaN -> INT_MIN), keep the low 16 bits.
@@ -136,6 +157,12 @@ hipError_t launch_mix_c64(const float2* x, long long n, double w, double sr, lon
 
 hipError_t launch_scale_c64(const float2* x, long long n, float s, float2* y, hipStream_t st) {
   hipLaunchKernelGGL(scale_c64, dim3(ew_grid(n)), dim3(256), 0, st, x, n, s, y);
+  return hipGetLastError();
+}
+
+hipError_t launch_fir_part_accum(const float2* z, long long nz, long long off, int D, long long ny,
+                                 int first, float2* y, hipStream_t st) {
+  hipLaunchKernelGGL(fir_part_accum, dim3(ew_grid(ny)), dim3(256), 0, st, z, nz, off, D, ny, first, y);
   return hipGetLastError();
 }
 

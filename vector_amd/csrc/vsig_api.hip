@@ -55,7 +55,13 @@ struct vsig_fir {
   long long hop;
   float2* Hs;
   float2* G = nullptr;   // D = 4 polyphase component filters (M = 1024)
+  // more than kFirPartTaps taps: undecimated parts of kFirPartTaps taps each,
+  // summed with their delays (fir_part_accum); z: one part's output
+  std::vector<vsig_fir*> parts;
+  float2* z = nullptr;
+  size_t zbytes = 0;
 };
+constexpr int kFirPartTaps = 8192;
 
 // A correlation template: L <= 8192 one spectrum of M points; longer
 // templates a spectrum per 8192-sample chunk (M = 16384), applied as a sum of
@@ -642,11 +648,28 @@ int vsig_psd_c64_dev(vsig_ctx* c, const void* x, int64_t n, int64_t stride, cons
                      float* sxx, int64_t nframes) {
   if (!c || !x || !win || !sxx) return fail(c, VSIG_E_INVALID, "null pointer");
   if (stride < 1) return fail(c, VSIG_E_INVALID, "stride must be >= 1");
-  if (!pow2_in(nfft, 64, kBigMax))
-    return fail(c, VSIG_E_UNSUPPORTED, "nfft must be a power of two in [64, 2^28]");
   if (nperseg < 1 || nperseg > nfft || hop < 1 || n < nperseg)
     return fail(c, VSIG_E_INVALID, "need 1 <= nperseg <= nfft, hop >= 1, n >= nperseg");
   if (nframes != (n - nperseg) / hop + 1) return fail(c, VSIG_E_INVALID, "nframes mismatch");
+  if (!pow2_in(nfft, 64, kBigMax)) {
+    // any other length: Bluestein per frame (bigfft.hip), |X|^2 stored by the
+    // transform's output stage; frames in batches of <= 256 MB of scratch
+    if (2LL * nfft - 1 > kBigMax) return fail(c, VSIG_E_UNSUPPORTED, "nfft above 2^27");
+    vsig_ctx::Chirp* ch;
+    int rc = chirp_plan(c, nfft, &ch);
+    if (rc) return rc;
+    long long fb = ch->M <= 16384 ? nframes : (256LL << 20) / (ch->M * 8);
+    if (fb < 1) fb = 1;
+    Timed t(c, "psd");
+    for (long long f0 = 0; f0 < nframes; f0 += fb) {
+      const long long nb = nframes - f0 < fb ? nframes - f0 : fb;
+      vsig::BigIn in{(const float2*)x + f0 * hop * stride, 0, hop * stride, stride, nperseg, nullptr,
+                     win, 0, 1.0f};
+      vsig::BigOut out{sxx + f0 * (long long)nfft, 4, nfft, nfft, nullptr, 0, scale, shift ? 1 : 0};
+      if ((rc = dft_any(c, nfft, nb, in, out, false))) return rc;
+    }
+    return VSIG_OK;
+  }
   if (nfft > 16384) {          // long frames: four-step FFT per frame (bigfft.hip)
     BigPlan bp;
     int rc = big_plan(c, nfft, &bp);
@@ -702,8 +725,21 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
   if (!c || !taps || !out) return fail(c, VSIG_E_INVALID, "null pointer");
   *out = nullptr;
   if (ntaps < 1 || decim < 1) return fail(c, VSIG_E_INVALID, "ntaps and decim must be >= 1");
+  if (ntaps > kFirPartTaps) {        // np.convolve has no length limit: parts
+    auto* f = new vsig_fir{c, ntaps, decim, 0, 0, nullptr};
+    for (int j = 0; j * kFirPartTaps < ntaps; ++j) {
+      const int nt = ntaps - j * kFirPartTaps < kFirPartTaps ? ntaps - j * kFirPartTaps : kFirPartTaps;
+      vsig_fir* p = nullptr;
+      const int rc = vsig_fir_create(c, static_cast<const float2*>(taps) + (size_t)j * kFirPartTaps, nt, 1, &p);
+      if (rc) { vsig_fir_free(f); return rc; }
+      f->parts.push_back(p);
+    }
+    f->M = f->parts[0]->M;
+    *out = f;
+    return VSIG_OK;
+  }
   const int M = os_size_fir(ntaps);
-  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "ntaps > 8192");
+  if (!M) return fail(c, VSIG_E_UNSUPPORTED, "no block size for ntaps");
   long long hop = ((long long)M - (ntaps - 1)) / decim * decim;
   if (hop < 1) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
   float2* hd = nullptr;
@@ -732,6 +768,8 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
 void vsig_fir_free(vsig_fir* f) {
   if (!f) return;
   (void)hipStreamSynchronize(f->ctx->stream);
+  for (vsig_fir* p : f->parts) vsig_fir_free(p);
+  (void)hipFree(f->z);
   (void)hipFree(f->Hs);
   (void)hipFree(f->G);
   delete f;
@@ -746,6 +784,18 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
   if (ny != (n + f->decim - 1) / f->decim) return fail(c, VSIG_E_INVALID, "ny != ceil(n/decim)");
   const float2* tw;
   int rc;
+  if (!f->parts.empty()) {
+    if (mix) return fail(c, VSIG_E_UNSUPPORTED, "fused mixer needs ntaps <= 256 (mix first)");
+    const long long nz = nhist + n;
+    if ((rc = ensure_buf(c, reinterpret_cast<void**>(&f->z), &f->zbytes, (size_t)nz * sizeof(float2))))
+      return rc;
+    for (size_t j = 0; j < f->parts.size(); ++j) {
+      if ((rc = fir_exec(f->parts[j], x, 0, nz, f->z, nz, nullptr))) return rc;
+      HIPCHK(c, vsig::launch_fir_part_accum(f->z, nz, nhist - (long long)j * kFirPartTaps, f->decim, ny,
+                                            j == 0, (float2*)y, c->stream));
+    }
+    return VSIG_OK;
+  }
   if (f->M == 1024 && (f->decim == 2 || f->decim == 4)) {
     // decimation in the frequency domain: M/D-point inverse transforms
     const float2* twd;

@@ -187,11 +187,13 @@ struct BigIn {                 // operand n of frame f
 };
 struct BigOut {                // natural-order result n of frame f
   void* dst;
-  int kind;                    // 0 complex64, 1 complex128, 2 float64 real part, 3 complex64 real part
+  int kind;                    // 0 complex64, 1 complex128, 2 float64 real part, 3 complex64 real part,
+                               // 4 float32 |X|^2 * scale (PSD), at (n + nout/2) % nout if shift
   long long fstride, nout;
   const float2* chirp;         // optional * chirp[n], then conj
   int conj;
   float scale;
+  int shift = 0;
 };
 void bigfft_split(long long M, int* N1, int* N2);
 hipError_t launch_bf_chirp(long long N, long long M, float2* c, float2* b, hipStream_t st);
@@ -220,6 +222,8 @@ hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* 
 hipError_t launch_mix_c64(const float2* x, long long n, double w, double sr, long long i0, float2* y,
                           hipStream_t st);
 hipError_t launch_scale_c64(const float2* x, long long n, float s, float2* y, hipStream_t st);
+hipError_t launch_fir_part_accum(const float2* z, long long nz, long long off, int D, long long ny,
+                                 int first, float2* y, hipStream_t st);
 hipError_t launch_wv_quantize(const float2* x, long long n, float norm, short* out, hipStream_t st);
 hipError_t launch_planar_to_c64(int mi_type, const void* re, const void* im, long long n, float2* y,
                                 hipStream_t st);
