@@ -243,15 +243,9 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-refine", action="store_true",
                     help="skip the correlator's exact-argmax refine pass (A/B only)")
-    ap.add_argument("--pipeline", type=int, default=1,
-                    help="sub-chunks per step: FIR / PSD / xcorr overlap on three HIP streams")
-    ap.add_argument("--serial", action="store_true",
-                    help="run the --pipeline sub-chunks in order on one stream (cache reuse)")
     ap.add_argument("--freq-shift", type=float, default=0.0,
                     help="NCO mixer (apply_frequency_shift) fused into the FIR loads, Hz")
     ap.add_argument("--sample-rate", type=float, default=2e9, help="for --freq-shift (config 5: 2 GS/s)")
-    ap.add_argument("--three-streams", action="store_true",
-                    help="FIR / PSD / xcorr on their own HIP streams (default: one stream)")
     ap.add_argument("--nchan", type=int, default=64)
     ap.add_argument("--branch-taps", type=int, default=16)
     ap.add_argument("--launcher-selftest", default=None, help=argparse.SUPPRESS)
@@ -293,8 +287,6 @@ def main():
     if args.no_refine:
         ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, b"refine", 0), "refine")
     cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=args.nfft, template=tmpl,
-                      pipeline=args.pipeline, serial=args.serial,
-                      one_stream=not args.three_streams,
                       freq_shift=args.freq_shift, sample_rate=args.sample_rate)
     be = HipBackend(cfg, local)
     chain = StreamChain(cfg, be, rank, world)
@@ -442,7 +434,6 @@ def main():
                    "ntaps": args.ntaps, "decim": decim, "nfft": args.nfft,
                    "template": args.template,
                    "parallelism": f"time-chunk x{world} (RCCL halos)",
-                   "pipeline": args.pipeline, "serial": args.serial,
                    "freq_shift": args.freq_shift, "refine": not args.no_refine},
         "roofline": roof,
         "cpu_baseline": cpu,

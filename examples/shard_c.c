@@ -153,6 +153,9 @@ int main(int argc, char** argv) {
     design(world);
     char id[128];
     if (rank == 0) {
+      /* IDFILE must be a fresh path per run: ranks > 0 take the first file
+       * they find there, so a stale one would make them join an old id */
+      remove(file);
       if (vsig_rccl_unique_id(id)) { fprintf(stderr, "no RCCL\n"); return 2; }
       char tmp[4096];
       snprintf(tmp, sizeof tmp, "%s.tmp", file);
@@ -177,6 +180,6 @@ int main(int argc, char** argv) {
     vsig_rccl_comm_destroy(comm);
     return a.ok ? 0 : 1;
   }
-  fprintf(stderr, "usage: shard_c loopback W | shard_c rccl RANK WORLD IDFILE\n");
+  fprintf(stderr, "usage: shard_c loopback W | shard_c rccl RANK WORLD IDFILE (a fresh path per run)\n");
   return 2;
 }

@@ -86,11 +86,20 @@ int vsig_synchronize(vsig_ctx* ctx);
 /* Options of the correlators' exact-argmax refine pass (refine.hip):
  *   "refine"          1 (default): after every correlation, the outputs whose
  *                     fp32 |c| lies within the band below the fp32 maximum are
- *                     recomputed by direct sums in double precision (a
- *                     compensated dot product for the final near-ties), in the
- *                     operands' own precision, and the record's peak / index
- *                     replaced -- np.argmax over numpy's complex128 sums;
- *                     0: the fp32 FFT result only;
+ *                     recomputed by direct sums in double precision, and the
+ *                     ones that can be the maximum once more in numpy's own
+ *                     operation order (OpenBLAS zdotu + numpy's complex abs),
+ *                     in the operands' own precision; the record's peak /
+ *                     index are replaced by numpy's -- np.argmax over
+ *                     np.abs(np.correlate) in complex128, to the bit;
+ *                     0: the fp32 FFT result only -- for the fused correlators
+ *                     (M >= 16384) the peak is then |c| with the low 6 mantissa
+ *                     bits of |c|^2 replaced by the output's rank in its thread
+ *                     (up to 3.8e-6 relative low; near-ties within 2^-17
+ *                     decided by that rank, not by the lowest index);
+ *   "blas_threads"    OpenBLAS threads of the numpy being matched (default 1;
+ *                     the Python front end sets numpy's own): its zdotu splits
+ *                     sums of more than 10000 terms into that many chunks;
  *   "refine_eps_ppm"  the band, relative to max |c| (default 1000 = 1e-3; the
  *                     fp32 correlation error is ~1e-8 of |p| |s_segment|);
  *   "refine_cap"      most outputs revisited (default 2^20); beyond it the

@@ -109,6 +109,54 @@ def test_native_chain_loopback_ranks(gpu, world, decim):
         assert pk[2] == pytest.approx(p1[2], rel=1e-5)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_native_chain_loopback_multi_step(gpu, world):
+    """Three steps per rank with the preamble at a different global offset each
+    time (re-loaded inputs): the loopback's halo boxes and peak gather rounds
+    are reused across steps, and every step reports its own lag on every rank."""
+    from vector_amd.shard import Loopback, NativeChain
+    n, L, decim = 1 << 17, 700, 4
+    N = world * n
+    taps = scipy.signal.firwin(255, 0.2).astype(np.float32)
+    pre = ref.qpsk_preamble(L * decim, seed=21)
+    tmpl = np.convolve(pre, taps)[: L * decim][::decim].astype(np.complex64)
+    base = ref.synth_iq(N, seed=22)
+    k0s = [(n // decim - L // 2) * decim, 1000 * decim, (N // decim - L - 50) * decim]
+    xs = []
+    for k in k0s:
+        x = base.copy()
+        x[k: k + L * decim] += 3 * pre
+        xs.append(x)
+    lb = Loopback(world)
+    res, errs = [None] * world, []
+
+    def rank_main(r):
+        try:
+            st = torch.cuda.Stream()
+            with torch.cuda.stream(st):
+                ch = NativeChain(_cfg(n, taps, decim, tmpl), 0, r, world, lb.transport(r))
+                got = []
+                for x in xs:
+                    ch.load(torch.from_numpy(x[r * n:(r + 1) * n]).cuda())
+                    ch.step()
+                    got.append(ch.global_peak())
+                st.synchronize()
+                res[r] = got
+                del ch
+        except Exception as e:      # surfaced below
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    for r in range(world):
+        assert [g[1] for g in res[r]] == [k // decim for k in k0s]
+        assert res[r] == res[0]
+
+
 def test_native_chain_rccl_world1(gpu):
     from vector_amd._lib import Transport
     from vector_amd.shard import NativeChain

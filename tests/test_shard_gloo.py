@@ -62,8 +62,12 @@ def make_case(world, n_local=4096, decim=2, nfft=256, ntaps=31, L=100, k0=None, 
     return x, taps, pre, k0, y_full
 
 
-def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, serial=False,
-            freq_shift=0.0):
+def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, freq_shift=0.0, k0s=None,
+            read_every=True):
+    """One rank.  k0s: the preamble's global offset at each step (one step per
+    entry; default: make_case's single step); read_every: global_peak() after
+    every step (else only after the last: the double-buffered all-gather
+    records of earlier steps are reused underneath)."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -71,30 +75,35 @@ def _worker(rank, world, port, n_local, decim, nfft, ntaps, L, q, pipeline=1, se
         x, taps, pre, k0, _ = make_case(world, n_local, decim, nfft, ntaps, L,
                                         freq_shift=freq_shift)
         cfg = ChainConfig(n_local=n_local, taps=taps, decim=decim, nfft=nfft, template=pre,
-                          pipeline=pipeline, serial=serial, freq_shift=freq_shift,
-                          sample_rate=SR)
-        be = OracleBackend(cfg)
+                          freq_shift=freq_shift, sample_rate=SR)
+        plant = [k0]
 
         class PlantingBackend(OracleBackend):
-            """Adds the preamble to the filtered stream at global k0 (as the
+            """Adds the preamble to the filtered stream at global plant[0] (as the
             single-stream reference does) before the PSD / xcorr stages."""
             def fir_into(self, x_ext, nhist, y, i0=None):
                 super().fir_into(x_ext, nhist, y, i0)
                 nyk = y.shape[0]
-                start = (y.data_ptr() - ch_holder[0].y_ext.data_ptr()) // 8   # sub-chunk offset
+                start = (y.data_ptr() - ch_holder[0].y_ext.data_ptr()) // 8   # offset in the chunk
                 lo = rank * (n_local // decim) + start
                 hi = lo + nyk
-                a, b = max(lo, k0), min(hi, k0 + L)
+                k = plant[0]
+                a, b = max(lo, k), min(hi, k + L)
                 if a < b:
-                    y[a - lo:b - lo] += torch.from_numpy((6 * pre[a - k0:b - k0]).astype(np.complex64))
+                    y[a - lo:b - lo] += torch.from_numpy((6 * pre[a - k:b - k]).astype(np.complex64))
 
         ch_holder = []
-        be = PlantingBackend(cfg)
-        ch = StreamChain(cfg, be, rank, world)
+        ch = StreamChain(cfg, PlantingBackend(cfg), rank, world)
         ch_holder.append(ch)
         ch.x.copy_(torch.from_numpy(x[rank * n_local:(rank + 1) * n_local]))
-        ch.step()
-        q.put((rank, ch.y.numpy().copy(), ch.sxx.numpy().copy(), ch.global_peak()))
+        peaks = []
+        steps = k0s if k0s is not None else [k0]
+        for j, k in enumerate(steps):
+            plant[0] = k
+            ch.step()
+            if read_every or j == len(steps) - 1:
+                peaks.append(ch.global_peak())
+        q.put((rank, ch.y.numpy().copy(), ch.sxx.numpy().copy(), peaks))
     finally:
         dist.destroy_process_group()
 
@@ -107,23 +116,13 @@ def free_port():
     return p
 
 
-@pytest.mark.parametrize("world,pipeline,serial,decim,L,freq_shift", [
-    (2, 1, False, 2, 100, 0.0), (3, 1, False, 2, 100, 0.0), (2, 4, False, 2, 100, 0.0),
-    (1, 4, False, 2, 100, 0.0), (2, 4, True, 2, 100, 0.0), (3, 2, True, 2, 100, 0.0),
-    (2, 1, False, 1, 100, 0.0), (3, 1, False, 1, 300, 0.0), (2, 4, False, 1, 450, 0.0),
-    (3, 1, False, 2, 100, FS), (2, 4, True, 2, 100, FS)])
-def test_sharded_chain_matches_single_stream(world, pipeline, serial, decim, L, freq_shift):
-    """decim 1: the left halo's split at ntaps-1 outputs; long templates (L up
-    to 450, a sub-chunk of 512 filtered samples at pipeline 4) widen the right
-    halo.  freq_shift: the mixer before the FIR, phase from the global sample
-    index on every rank."""
-    n_local, nfft, ntaps = 4096, 256, 31
+def _run(world, n_local, decim, nfft, ntaps, L, freq_shift=0.0, k0s=None, read_every=True):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = free_port()
     procs = [ctx.Process(target=_worker,
-                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, pipeline, serial,
-                               freq_shift))
+                         args=(r, world, port, n_local, decim, nfft, ntaps, L, q, freq_shift, k0s,
+                               read_every))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -134,6 +133,18 @@ def test_sharded_chain_matches_single_stream(world, pipeline, serial, decim, L, 
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    return res
+
+
+@pytest.mark.parametrize("world,decim,L,freq_shift", [
+    (2, 2, 100, 0.0), (3, 2, 100, 0.0), (1, 2, 100, 0.0), (2, 1, 100, 0.0), (3, 1, 300, 0.0),
+    (2, 1, 450, 0.0), (3, 2, 100, FS), (2, 2, 100, FS)])
+def test_sharded_chain_matches_single_stream(world, decim, L, freq_shift):
+    """decim 1: the left halo's split at ntaps-1 outputs; long templates (L up
+    to 450) widen the right halo.  freq_shift: the mixer before the FIR, phase
+    from the global sample index on every rank."""
+    n_local, nfft, ntaps = 4096, 256, 31
+    res = _run(world, n_local, decim, nfft, ntaps, L, freq_shift)
     x, taps, pre, k0, y_full = make_case(world, n_local, decim, nfft, ntaps, L,
                                          freq_shift=freq_shift)
     ny = n_local // decim
@@ -144,11 +155,40 @@ def test_sharded_chain_matches_single_stream(world, pipeline, serial, decim, L, 
     np.testing.assert_allclose(s_cat, S.T, rtol=1e-5, atol=1e-6 * S.max())
     i, lag, peak, s1, s2, conf = ref.xcorr_peak(y_full, pre, "valid")
     for r in range(world):
-        m, gi, a, b, nout = res[r][2]
+        m, gi, a, b, nout = res[r][2][0]
         assert gi == lag == k0                                   # exact, on every rank
         assert nout == world * ny - L + 1
         assert m == pytest.approx(peak, rel=1e-6)
         assert a == pytest.approx(s1, rel=1e-6) and b == pytest.approx(s2, rel=1e-6)
+
+
+@pytest.mark.parametrize("world,read_every", [(2, True), (3, True), (3, False), (2, False)])
+def test_sharded_chain_multi_step_peaks(world, read_every):
+    """Five steps with the preamble planted at a different global offset each
+    step (on either side of the rank boundaries): the double-buffered,
+    asynchronous peak all-gather must give every step's own global peak --
+    global_peak() after each step, or only after the last one (the slots of
+    earlier steps reused underneath)."""
+    n_local, decim, nfft, ntaps, L = 4096, 2, 256, 31, 100
+    ny = n_local // decim
+    k0s = [ny - L // 2, 300, world * ny - L - 7, ny + 900, 2 * ny // 3]
+    res = _run(world, n_local, decim, nfft, ntaps, L, k0s=k0s, read_every=read_every)
+    x, taps, pre, _, _ = make_case(world, n_local, decim, nfft, ntaps, L)
+    y0 = np.convolve(x, taps)[: world * n_local][::decim].astype(np.complex64)
+    want = []
+    for k in k0s:
+        y = y0.copy()
+        y[k:k + L] += 6 * pre
+        want.append(ref.xcorr_peak(y, pre, "valid"))
+    if not read_every:
+        want = want[-1:]
+    for r in range(world):
+        got = res[r][2]
+        assert len(got) == len(want)
+        for (m, gi, a, b, nout), w in zip(got, want):
+            assert gi == w[1]
+            assert m == pytest.approx(w[2], rel=1e-6)
+            assert a == pytest.approx(w[3], rel=1e-6)
 
 
 def test_combine_peaks_tie_lowest_index():

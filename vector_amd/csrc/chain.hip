@@ -322,11 +322,15 @@ int vsig_rccl_comm_init(int32_t world, int32_t rank, const char id[128], int32_t
   if (!id || !comm || world < 1 || rank < 0 || rank >= world) return VSIG_E_INVALID;
   Rccl& r = rccl();
   if (!r.ok) return VSIG_E_UNSUPPORTED;
-  if (hipSetDevice(device) != hipSuccess) return VSIG_E_HIP;
+  // the communicator binds to the current device: set it for the call only
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess || hipSetDevice(device) != hipSuccess) return VSIG_E_HIP;
   nccl_uid u;
   memcpy(u.internal, id, 128);
   nccl_comm cm = nullptr;
-  if (r.CommInitRank(&cm, world, u, rank)) return VSIG_E_HIP;
+  const int rc = r.CommInitRank(&cm, world, u, rank);
+  (void)hipSetDevice(prev);
+  if (rc) return VSIG_E_HIP;
   *comm = cm;
   return VSIG_OK;
 }

@@ -402,7 +402,8 @@ __device__ __forceinline__ int bfly(int t, int b) {
 // A plan with its exchange geometry set (see above).
 template <class P, int M0, int ML, int S = 5, int U = 0>
 struct Lanes : P {
-  static_assert(M0 != kMapPair || P::TF == 64, "the pair map is for one-wave frames");
+  static_assert((M0 != kMapPair && ML != kMapPair) || P::TF == 64,
+                "the pair map is for one-wave frames (not a permutation of t >= 64)");
   static_assert((M0 != kMapIlv || P::E / P::R[0] == 2) && (ML != kMapIlv || P::E / P::RL == 2),
                 "the interleaved map pairs two butterflies per thread");
   static_assert(P::TF % 64 == 0 && (P::N / P::R[0]) % 32 == 0, "maps permute 32-lane runs");

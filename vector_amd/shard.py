@@ -25,7 +25,6 @@ unit-tested on CPU with gloo; the product backend is HipBackend (libvsig.so).
 """
 from __future__ import annotations
 
-import contextlib
 from dataclasses import dataclass
 
 import numpy as np
@@ -44,25 +43,15 @@ class ChainConfig:
     nfft: int = 8192             # PSD frame = hop (non-overlapping)
     template: np.ndarray | None = None   # sync preamble (None: no xcorr stage)
     window: str = "hann"
-    pipeline: int = 1            # sub-chunks per step (FIR / PSD / xcorr overlap on 3 streams)
-    serial: bool = False         # sub-chunks in order on one stream: FIR(k+1), PSD(k), xcorr(k)
-                                 # (a sub-chunk's filtered samples are re-read while cache-resident)
     freq_shift: float = 0.0      # apply_frequency_shift before the FIR (fused into its loads),
     sample_rate: float = 1.0     # phase from the global sample index (utils.py:120-127)
-    one_stream: bool = True      # pipeline == 1: all stages on the caller's stream (the PSD and
-                                 # correlator do not overlap anyway; saves the cross-stream waits)
 
     def validate(self, world: int):
         ny = self.n_local // self.decim
-        K = self.pipeline
-        if K < 1 or self.n_local % K:
-            raise ValueError("n_local must be a multiple of pipeline")
-        if self.n_local % (self.decim * K):
-            raise ValueError("n_local must be a multiple of decim * pipeline")
-        if (ny // K) % self.nfft:
-            raise ValueError("n_local/decim/pipeline must be a multiple of nfft (frames never straddle chunks)")
-        if self.template is not None and K > 1 and ny // K < len(self.template) - 1:
-            raise ValueError("sub-chunk shorter than the template halo")
+        if self.n_local % self.decim:
+            raise ValueError("n_local must be a multiple of decim")
+        if ny % self.nfft:
+            raise ValueError("n_local/decim must be a multiple of nfft (frames never straddle chunks)")
         if self.template is not None and world > 1 and ny < len(self.template) - 1:
             raise ValueError("chunk shorter than the template halo")
         if world > 1 and self.n_local < len(self.taps) - 1:
@@ -100,34 +89,9 @@ class HipBackend:
         self.scale = float(1.0 / float(np.sum(w, dtype=np.float64)) ** 2)
         self.nfft = cfg.nfft
         self.freq_shift, self.sample_rate = cfg.freq_shift, cfg.sample_rate
-        self.lanes = {k: torch.cuda.Stream(device=self.dev) for k in ("fir", "psd", "xcorr")}
 
     def empty(self, n, dtype=torch.complex64):
         return torch.zeros(n, dtype=dtype, device=self.dev)
-
-    # stream "lanes": the three stages of a pipelined step run on their own
-    # HIP streams, ordered by events (FIR(k) -> PSD(k); FIR(k+1) -> xcorr(k)).
-    def lane(self, name):
-        return torch.cuda.stream(self.lanes[name])
-
-    def record(self):
-        ev = torch.cuda.Event()
-        ev.record()
-        return ev
-
-    def wait(self, ev):
-        if ev is not None:
-            torch.cuda.current_stream(self.dev).wait_event(ev)
-
-    def join(self):
-        cur = torch.cuda.current_stream(self.dev)
-        for st in self.lanes.values():
-            cur.wait_stream(st)
-
-    def fork(self):
-        cur = torch.cuda.current_stream(self.dev)
-        for st in self.lanes.values():
-            st.wait_stream(cur)
 
     def fir_into(self, x_ext, nhist, y, i0=0):
         """i0: global sample index of x_ext[0] (the mixer's phase origin)."""
@@ -151,19 +115,6 @@ class HipBackend:
         self.xc(s, "valid", peak=rec)
 
 
-def _lane(be, name):
-    return be.lane(name) if hasattr(be, "lane") else contextlib.nullcontext()
-
-
-def _record(be):
-    return be.record() if hasattr(be, "record") else None
-
-
-def _wait(be, ev):
-    if hasattr(be, "wait"):
-        be.wait(ev)
-
-
 class StreamChain:
     """One rank's part of the sharded chain (world = 1: the plain chain)."""
 
@@ -180,9 +131,8 @@ class StreamChain:
         # peak records, double-buffered: the all-gather of step k runs behind
         # step k + 1 (it is waited for only before step k + 2 reuses its slot,
         # or by global_peak); every rank's records land in place (no copies)
-        K = cfg.pipeline
-        self._recs = backend.empty(2 * 4 * K, torch.float64).view(2, K, 4)
-        self._rows = backend.empty(2 * 4 * K * world, torch.float64).view(2, world * K, 4)
+        self._recs = backend.empty(2 * 4, torch.float64).view(2, 4)
+        self._rows = backend.empty(2 * 4 * world, torch.float64).view(2, world * 4)
         self._gather = [None, None]
         self._slot = 1
         self.peak_rows = None
@@ -197,8 +147,8 @@ class StreamChain:
         return self.y_ext[: self.ny]
 
     @property
-    def recs(self):
-        """This step's peak records (one per sub-chunk)."""
+    def rec(self):
+        """This step's peak record."""
         return self._recs[self._slot]
 
     def _begin_step(self):
@@ -209,9 +159,9 @@ class StreamChain:
 
     def _gather_peaks(self):
         rows = self._rows[self._slot]
-        self._gather[self._slot] = dist.all_gather_into_tensor(rows, self.recs, group=self.group,
+        self._gather[self._slot] = dist.all_gather_into_tensor(rows, self.rec, group=self.group,
                                                                async_op=True)
-        return list(rows.view(self.world, self.cfg.pipeline, 4).unbind(0))
+        return list(rows.view(self.world, 4).unbind(0))
 
     def _exchange_start(self, send, dst, recv, src):
         ops = []
@@ -237,8 +187,8 @@ class StreamChain:
         else:
             be.fir_into(x, self.hist, y)
 
-    def _fir_first(self, be, nk, nyk):
-        """FIR of sub-chunk 0 with the left-halo exchange hidden behind it:
+    def _fir_first(self, be):
+        """FIR of the chunk with the left-halo exchange hidden behind it:
         outputs from a decimation-aligned s >= ntaps-1 on need only the rank's
         own samples and are filtered while the halo is in flight; the first
         s outputs follow once it has landed."""
@@ -248,72 +198,29 @@ class StreamChain:
         def run(a, b):
             self._fir(be, a, b, self.y_ext[a // D: b // D])
         if not (w > 1 and hist > 0):
-            run(0, nk)
+            run(0, n)
             return
         reqs = self._exchange_start(self.x_ext[n: n + hist] if r < w - 1 else None,
                                     r + 1 if r < w - 1 else None,
                                     self.x_ext[: hist] if r > 0 else None,
                                     r - 1 if r > 0 else None)
         s = -(-hist // D) * D
-        if s < nk:
-            run(s, nk)
+        if s < n:
+            run(s, n)
         self._exchange_wait(reqs)
-        run(0, min(s, nk))
+        run(0, min(s, n))
 
     def step(self):
+        """One step, every stage on the current stream: FIR (left halo hidden
+        behind its bulk), the right-halo exchange started behind it, the PSD
+        while the halo is in flight, then the correlator once it has landed,
+        then the peak records' all-gather (asynchronous, see __init__).
+        (Three-stream and sub-chunked pipelines measured slower on MI355X:
+        DESIGN.md section 5.)"""
         self._begin_step()
-        if self.cfg.serial:
-            return self._step_serial()
-        if self.cfg.pipeline == 1 and self.cfg.one_stream:
-            return self._step_single()
-        r, w, K = self.rank, self.world, self.cfg.pipeline
+        r, w, ny, L = self.rank, self.world, self.ny, self.L
         be = self.be
-        n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
-        nk, nyk = n // K, ny // K
-        if hasattr(be, "fork"):
-            be.fork()
-        ev_fir, ev_halo = [], None
-        with _lane(be, "fir"):
-            for k in range(K):                  # 1-2. left halo + FIR (+ decimation), sub-chunk k
-                if k == 0:
-                    self._fir_first(be, nk, nyk)
-                else:
-                    self._fir(be, k * nk, (k + 1) * nk, self.y_ext[k * nyk: (k + 1) * nyk])
-                ev_fir.append(_record(be))
-                if k == 0 and w > 1 and L > 1:  # 3. right halo of the filtered stream
-                    self._exchange(self.y_ext[: L - 1] if r > 0 else None,
-                                   r - 1 if r > 0 else None,
-                                   self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
-                                   r + 1 if r < w - 1 else None)
-                    ev_halo = _record(be)
-        for k in range(K):
-            with _lane(be, "psd"):              # 4. PSD of sub-chunk k
-                _wait(be, ev_fir[k])
-                be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
-            if L:                               # 5. sync correlation of sub-chunk k
-                with _lane(be, "xcorr"):
-                    last = k == K - 1
-                    _wait(be, ev_fir[k + 1] if not last else ev_fir[k])
-                    if last and ev_halo is not None:
-                        _wait(be, ev_halo)
-                    halo = (L - 1) if (not last or r < w - 1) else 0
-                    be.xcorr_peak(self.y_ext[k * nyk: (k + 1) * nyk + halo], self.recs[k])
-        if hasattr(be, "join"):
-            be.join()
-        if L:
-            if w > 1:                           # 6. global peak records
-                self.peak_rows = self._gather_peaks()
-            else:
-                self.peak_rows = [self.recs]
-
-    def _step_single(self):
-        """One sub-chunk, every stage on the current stream: FIR (left halo
-        hidden behind its bulk), the right-halo exchange started behind it,
-        the PSD while the halo is in flight, then the correlator once it has
-        landed, then the peak records."""
-        r, w, n, ny, L = self.rank, self.world, self.cfg.n_local, self.ny, self.L
-        be = self.be
-        self._fir_first(be, n, ny)
+        self._fir_first(be)
         reqs = []
         if w > 1 and L > 1:
             reqs = self._exchange_start(self.y_ext[: L - 1] if r > 0 else None,
@@ -321,55 +228,11 @@ class StreamChain:
                                         self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
                                         r + 1 if r < w - 1 else None)
         be.psd_into(self.y_ext[: ny], self.sxx)
+        self._exchange_wait(reqs)
         if L:
-            self._exchange_wait(reqs)
             halo = (L - 1) if r < w - 1 else 0
-            be.xcorr_peak(self.y_ext[: ny + halo], self.recs[0])
-            if w > 1:
-                self.peak_rows = self._gather_peaks()
-            else:
-                self.peak_rows = [self.recs]
-        else:
-            self._exchange_wait(reqs)
-
-    def _step_serial(self):
-        """The same step with the sub-chunks run in order on the current stream,
-        PSD(k) and xcorr(k) right after FIR(k+1) (xcorr(k) needs the first L-1
-        filtered samples of sub-chunk k+1): each sub-chunk's filtered stream is
-        re-read soon after it is written instead of a whole chunk later."""
-        r, w, K = self.rank, self.world, self.cfg.pipeline
-        be = self.be
-        n, hist, ny, L = self.cfg.n_local, self.hist, self.ny, self.L
-        nk, nyk = n // K, ny // K
-
-        def fir(k):
-            if k == 0:                          # with the left-halo exchange
-                self._fir_first(be, nk, nyk)
-                return
-            self._fir(be, k * nk, (k + 1) * nk, self.y_ext[k * nyk: (k + 1) * nyk])
-
-        def consume(k):
-            be.psd_into(self.y_ext[k * nyk: (k + 1) * nyk], self.sxx[k * nyk: (k + 1) * nyk])
-            if L:
-                last = k == K - 1
-                halo = (L - 1) if (not last or r < w - 1) else 0
-                be.xcorr_peak(self.y_ext[k * nyk: (k + 1) * nyk + halo], self.recs[k])
-
-        fir(0)
-        if w > 1 and L > 1:                     # right halo of the filtered stream
-            self._exchange(self.y_ext[: L - 1] if r > 0 else None,
-                           r - 1 if r > 0 else None,
-                           self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
-                           r + 1 if r < w - 1 else None)
-        for k in range(1, K):
-            fir(k)
-            consume(k - 1)
-        consume(K - 1)
-        if L:
-            if w > 1:
-                self.peak_rows = self._gather_peaks()
-            else:
-                self.peak_rows = [self.recs]
+            be.xcorr_peak(self.y_ext[: ny + halo], self.rec)
+            self.peak_rows = self._gather_peaks() if w > 1 else [self.rec]
 
     def global_peak(self):
         """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step."""
@@ -377,14 +240,10 @@ class StreamChain:
         if work is not None:
             work.wait()
         rows = []
-        nyk = self.ny // self.cfg.pipeline
         for r, t in enumerate(self.peak_rows):
-            h = t.detach().cpu().reshape(-1, 4)
-            hi = h.view(torch.int64)
-            for k in range(h.shape[0]):
-                idx = int(hi[k, 1].item())
-                rows.append((float(h[k, 0]), r * self.ny + k * nyk + idx, float(h[k, 2]),
-                             float(h[k, 3])))
+            h = t.detach().cpu().reshape(4)
+            idx = int(h.view(torch.int64)[1].item())
+            rows.append((float(h[0]), r * self.ny + idx, float(h[2]), float(h[3])))
         m, i, s1, s2 = combine_peaks(np.array(rows, dtype=object))
         nout = self.world * self.ny - self.L + 1
         return m, i, s1, s2, nout
@@ -414,6 +273,7 @@ class Loopback:
         rc = self.lib.vsig_loopback_transport(self.h, int(rank), C.byref(t))
         if rc:
             raise ValueError(f"vsig_loopback_transport: {rc}")
+        t._owner = self          # t.user points into this loopback: keep it alive with t
         return t
 
     def __del__(self):
