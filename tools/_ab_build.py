@@ -24,6 +24,9 @@ VARIANTS = {
     "libvsig_unphased": ("VSIG_FFT_UNPHASED",),
     "libvsig_rg1024": ("VSIG_REFINE_G1=1024", "VSIG_REFINE_G2=256"),
     "libvsig_nol1tw": ("VSIG_NO_L1TW",),
+    "libvsig_rko1": ("VSIG_REFINE_KO=1",),
+    "libvsig_rko2": ("VSIG_REFINE_KO=2",),
+    "libvsig_rko3": ("VSIG_REFINE_KO=3",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

@@ -18,24 +18,20 @@
 //             is (a wave covers ob + wstep w + l + 64 (q % rsub) + stride
 //             (q / rsub), see xcorr.hip); for a stored c64 array, its
 //             64-output chunks holding one;
-//   stage 1 : every output of every item by a plain fp64 direct sum
-//             c[o] = sum_k a[i - (nv-1) + k] conj(v[k]), i = F + o, with the
-//             sum S of the products' component magnitudes; that bounds how far
-//             both this sum and numpy's own (below) lie from the exact value:
-//             |c| +- E, E = (n/8 + n/64 + T + 300) 2^-52 S + 2^-49 |c|; the
-//             largest lower end (|c| - E) by a 64-bit atomic max;
-//   stage 2 : the outputs whose upper end reaches that lower end, evaluated in
-//             numpy's own operation order -- np.correlate's complex128 dot is
-//             OpenBLAS zdotu (8 fma accumulators per component over complex
-//             k mod 8, a fixed add tree, a scalar fma tail, re = d0 - d1,
-//             im = d2 + d3; above 10000 terms split over T = blas_threads
-//             chunks added in order), |c| by numpy's complex abs (larger *
-//             sqrt(fma(r, r, 1)), r = smaller / larger) -- so every value is
-//             numpy's to the bit (oracle/npdot.c restates it on the CPU and
-//             tests/test_npdot_cpu.py pins it against numpy).  np.argmax's
-//             rule then applies as is: the max |c| and the lowest output index
-//             attaining it, by the last stage-2 block, which replaces the peak
-//             record's max / index (sums untouched);
+//   numpy   : every output of every item evaluated in numpy's own operation
+//             order -- np.correlate's complex128 dot is OpenBLAS zdotu (8 fma
+//             accumulators per component over complex k mod 8, a fixed add
+//             tree, a scalar fma tail, re = d0 - d1, im = d2 + d3; above 10000
+//             terms split over T = blas_threads chunks added in order), |c| by
+//             numpy's complex abs (larger * sqrt(fma(r, r, 1)), r = smaller /
+//             larger) -- so every value is numpy's to the bit (oracle/npdot.c
+//             restates it on the CPU, tests/test_npdot_cpu.py pins it against
+//             numpy).  np.argmax's rule then applies as is: the max |c| and the
+//             lowest output index attaining it, by the last block, which
+//             replaces the peak record's max / index (sums untouched).  The
+//             operand windows go through LDS (the whole block loads a tile,
+//             the 8 lanes of zdot's slots consume it), so the sequential fma
+//             chains do not wait on a memory round trip per step;
 //   patch   : optionally the refined values into a complex128 c.
 // All sizes on the device (no host synchronisation); more than `cap` items
 // leaves the record as the fp32 pass produced it and sets status = 1.
@@ -69,12 +65,11 @@ __device__ __forceinline__ void tap_range(long long i, long long na, long long n
 // Shared scratch header (zeroed before select: by the fused finalize, or a memset).
 struct RefineKeys {
   unsigned long long count;    // candidate items appended by select
-  unsigned long long max1;     // bits of the stage-1 max |c|^2 (>= 0: integer order)
-  unsigned long long max2;     // bits of the stage-2 max |c|^2
-  unsigned long long negidx;   // INT64_MAX - lowest output index attaining max2
+  unsigned long long unused1;
+  unsigned long long max2;     // bits of numpy's max |c| (>= 0: integer order)
+  unsigned long long unused3;
   unsigned long long status;   // 1: more than cap items (record left unrefined)
-  unsigned long long done;     // stage-2 blocks finished (the last one finishes)
-  unsigned long long nsurv;    // stage-2 survivors (listed in items while <= cap)
+  unsigned long long done;     // numpy-pass blocks finished (the last one finishes)
 };
 static_assert(sizeof(RefineKeys) <= 64, "the items follow the keys at +64 B");
 
@@ -137,6 +132,7 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     const long long hi = lo + f.chunk < f.nparts ? lo + f.chunk : f.nparts;
     double m = -1.0, s1 = 0.0, s2 = 0.0;
     long long mi = 0x7fffffffffffffffLL;
+#pragma unroll 8
     for (long long i = lo + tid; i < hi; i += 256) {
       const PeakPartial p = f.parts[i];
       betterd(m, mi, p.max2, p.idx);
@@ -189,9 +185,18 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
   for (int c = 0; c < nc; ++c) {
     const long long lo = (long long)clist[c] * f.chunk;
     const long long hi = lo + f.chunk < f.nparts ? lo + f.chunk : f.nparts;
-    for (long long pb = lo + (tid - lane); pb < hi; pb += 256) {   // uniform per wave
-      const long long p = pb + lane;
-      unsigned long long hits = __ballot(p < hi && f.parts[p].max2 >= t2);
+    constexpr int kPre = 8;                       // partial maxima loaded ahead
+    for (long long pb0 = lo + (tid - lane); pb0 < hi; pb0 += 256LL * kPre) {   // uniform per wave
+      double pm[kPre];
+#pragma unroll
+      for (int q = 0; q < kPre; ++q) {
+        const long long p = pb0 + 256LL * q + lane;
+        pm[q] = p < hi ? f.parts[p].max2 : -1.0;
+      }
+#pragma unroll 1
+      for (int q = 0; q < kPre; ++q) {
+      const long long pb = pb0 + 256LL * q;
+      unsigned long long hits = __ballot(pm[q] >= t2);
       // past the cap the refine is skipped anyway (status 1): stop appending
       // (a flat |c| puts every partial in the band)
       if (*(volatile unsigned long long*)&scount > (unsigned long long)f.cap) hits = 0;
@@ -214,6 +219,7 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
         j0 = __shfl(j0, 0);
         const unsigned long long j = j0 + __popcll(km & ((1ull << lane) - 1));
         if (take && (long long)j < f.cap) f.items[j] = item;
+      }
       }
     }
     __syncthreads();
@@ -267,276 +273,166 @@ __device__ __forceinline__ long long unit_output(const RefineGeom& g, long long 
   return item_output(g, item, qu, po);
 }
 
-// Stage 1: 64 / OUTS blocks per unit of 64 outputs (a wave item's row q, or
-// a column item), OUTS outputs each: thread (w, l) of a 16-wave block sums
-// output OUTS sub + (l mod OUTS) over tap chunk (64 / OUTS) w + l / OUTS of
-// kS1Waves 64 / OUTS (independent partial sums, loads unrolled 8-deep), the
-// chunk sums combined in LDS in chunk order.  OUTS = 16 for wave items (64
-// chunks: 8 load batches for 4096 taps), 4 for the 64x fewer column items
-// (256 chunks, 2 batches).  vals / idx / cv are indexed by u * 64 + o, u =
-// item slot * Q + q, o the output's place in the unit.
-template <class T>
-__device__ __forceinline__ void direct_sum(const T* __restrict__ a, const T* __restrict__ v,
-                                           long long abase, long long k0, long long k1,
-                                           double& re, double& im, double& sa) {
-  long long k = k0;
-  double r0 = 0, r1 = 0, i0 = 0, i1 = 0, s0 = 0, s1 = 0;
-  for (; k + 8 <= k1; k += 8) {
-    double2 x[8], y[8];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) { x[j] = ld2<T>(a, abase + k + j); y[j] = ld2<T>(v, k + j); }
-#pragma unroll
-    for (int j = 0; j < 8; j += 2) {
-      r0 = fma(x[j].x, y[j].x, r0); r0 = fma(x[j].y, y[j].y, r0);
-      i0 = fma(x[j].y, y[j].x, i0); i0 = fma(-x[j].x, y[j].y, i0);
-      s0 = fma(fabs(x[j].x) + fabs(x[j].y), fabs(y[j].x) + fabs(y[j].y), s0);
-      r1 = fma(x[j + 1].x, y[j + 1].x, r1); r1 = fma(x[j + 1].y, y[j + 1].y, r1);
-      i1 = fma(x[j + 1].y, y[j + 1].x, i1); i1 = fma(-x[j + 1].x, y[j + 1].y, i1);
-      s1 = fma(fabs(x[j + 1].x) + fabs(x[j + 1].y), fabs(y[j + 1].x) + fabs(y[j + 1].y), s1);
-    }
-  }
-  for (; k < k1; ++k) {
-    const double2 x = ld2<T>(a, abase + k), y = ld2<T>(v, k);
-    r0 = fma(x.x, y.x, r0); r0 = fma(x.y, y.y, r0);
-    i0 = fma(x.y, y.x, i0); i0 = fma(-x.x, y.y, i0);
-    s0 = fma(fabs(x.x) + fabs(x.y), fabs(y.x) + fabs(y.y), s0);
-  }
-  re = r0 + r1;
-  im = i0 + i1;
-  sa = s0 + s1;
-}
-
-// Half-width of the interval around a stage-1 |c| that holds both the exact
-// |c| and numpy's (see the header): n overlap terms, S the sum of the
-// products' component magnitudes (>= 1 ulp-scale error sources of both sums).
-__device__ __forceinline__ double np_band(long long n, int nthr, double S, double c1) {
-  const double m = (double)(n / 8 + n / 64 + nthr + 300);
-  return m * 0x1p-52 * S + 0x1p-49 * c1;
-}
-
-constexpr int kS1Waves = 16;
-
-template <class T, int OUTS>
-__global__ __launch_bounds__(kS1Waves * 64) void refine_stage1(const T* __restrict__ a, const T* __restrict__ v,
-                                                     RefineGeom g, const long long* __restrict__ items,
-                                                     long long cap, RefineKeys* __restrict__ keys,
-                                                     double* __restrict__ vals,
-                                                     long long* __restrict__ oidx,
-                                                     double2* __restrict__ cv) {
-  constexpr int kChunks = kS1Waves * 64 / OUTS;     // tap chunks per output
-  constexpr int kSplit = 64 / OUTS;                 // blocks per unit
-  const long long cnt = (long long)keys->count;
-  if (keys->status || cnt == 0) return;
-  const long long nunits = (cnt < cap ? cnt : cap) * g.Q;
-  const int l = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int ol = l & (OUTS - 1);                    // output within the block
-  const int ch = w * (64 / OUTS) + (l / OUTS);      // tap chunk
-  __shared__ double pr[kChunks][OUTS], pi[kChunks][OUTS], pa[kChunks][OUTS];
-  for (long long ub = blockIdx.x; ub < nunits * kSplit; ub += gridDim.x) {   // uniform per block
-    const long long u = ub / kSplit;
-    const int sub = (int)(ub - u * kSplit);
-    const long long item = items[u / g.Q];
-    const int q = (int)(u % g.Q);
-    const int po = sub * OUTS + ol;                 // output's place in the unit (0..63)
-    const long long o = unit_output(g, item, q, po);
-    double re = 0.0, im = 0.0, sa = 0.0;
-    long long k0 = 0, k1 = 0;
-    if (o >= 0) {
-      const long long i = g.F + o;
-      tap_range(i, g.na, g.nv, k0, k1);
-      const long long span = (k1 - k0 + kChunks - 1) / kChunks;      // this chunk's share
-      const long long q0 = k0 + ch * span;
-      const long long q1 = q0 + span < k1 ? q0 + span : k1;
-      if (q0 < q1) direct_sum<T>(a, v, i - (g.nv - 1), q0, q1, re, im, sa);
-    }
-    pr[ch][ol] = re;
-    pi[ch][ol] = im;
-    pa[ch][ol] = sa;
-    __syncthreads();
-    if (threadIdx.x < OUTS) {                       // lanes 0..OUTS-1 of wave 0 (chunk 0): output ol
-      re = 0.0;
-      im = 0.0;
-      sa = 0.0;
-#pragma unroll 8
-      for (int c = 0; c < kChunks; ++c) { re += pr[c][ol]; im += pi[c][ol]; sa += pa[c][ol]; }
-      // vals: the upper end of the output's interval, max1: the largest lower end
-      double up = -1.0, lo = -1.0;
-      if (o >= 0) {
-        const double c1 = sqrt(re * re + im * im);
-        const double E = np_band(k1 - k0, g.nthr, sa, c1);
-        up = c1 + E;
-        lo = c1 - E > 0.0 ? c1 - E : 0.0;
-      }
-      const long long e = u * 64 + po;
-      vals[e] = up;
-      oidx[e] = o;
-      cv[e] = make_double2(re, im);
-      double wm = lo;
-#pragma unroll
-      for (int off = OUTS / 2; off > 0; off >>= 1) {
-        const double o2 = __shfl_xor(wm, off);
-        wm = o2 > wm ? o2 : wm;
-      }
-      if (ol == 0 && wm >= 0.0) atomicMax(&keys->max1, (unsigned long long)__double_as_longlong(wm));
-    }
-    __syncthreads();
-  }
-}
-
-// Stage 2: numpy's value of every output whose interval reaches the largest
-// lower end (see the header), then np.argmax.  One 8-lane group per output
-// (a wave takes up to 8 outputs): lane s of the group runs OpenBLAS zdot
-// kernel slot s -- the four fma chains over complex k = s mod 8 of the block
-// part n8 = n & -8 of a chunk -- the add tree combines the slots exactly as
-// zdot_kernel_8 does ((s, s^2), then (s, s^4), then the two 128-bit halves:
-// s, s^1), and slot 0 runs the scalar tail.  Chunks (OpenBLAS threads, only
-// above 10000 terms) run one after another in the group and are added in
-// order onto zero, as zdotu_k does.  Every step is an IEEE double fma / add /
-// sub / div / sqrt, so the values are numpy's bit for bit.
-constexpr int kS2Threads = 1024;
+// One zdot_compute over chunk [c0, c0 + w) of output i's overlap (x = a +
+// ax, y = conj(v)), in numpy's order.  Tiles of kTile complex are staged by
+// the whole block into LDS as planar doubles (xr, xi, yr, -yi); lane
+// 8 comp + s (< 32) of wave 0 runs one of zdot_kernel_8's fma chains: slot s
+// (complex k = s mod 8 of the block part n8 = w & -8) of component comp (xr yr,
+// xi yi, xr yi, xi yr) -- one dependent fma per step, its operands two LDS
+// reads.  The add tree combines the slots as the kernel does ((s, s^2), then
+// (s, s^4), then the two 128-bit halves: s, s^1); lane 0 gathers the four
+// sums and runs the scalar tail.  Result in lane 0.
+#ifndef VSIG_REFINE_KO
+#define VSIG_REFINE_KO 0
+#endif
+constexpr int kNpThreads = 256;
+constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
 constexpr long long kBlasThreadMin = 10000;   // zdotu_k: threads only above this n
 
 template <class T>
-__device__ __forceinline__ double2 ldc(const T* p, long long i) { return ld2<T>(p, i); }
-
-// One zdot_compute over chunk [c0, c0 + w) of the overlap (x = a + ax, y =
-// conj(v)); the result in slot 0 (lane s == 0) of the group.
-template <class T>
 __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* __restrict__ v,
-                                              long long ax, long long c0, long long w, int s,
-                                              double& re, double& im) {
+                                              long long ax, long long c0, long long w,
+                                              double* lds, double& re, double& im) {
+  const int tid = threadIdx.x, s = tid & 7, comp = (tid >> 3) & 3;
+  double* xr = lds;
+  double* xi = lds + kTile;
+  double* yr = lds + 2 * kTile;
+  double* yn = lds + 3 * kTile;
+  const double* X = (comp == 0 || comp == 2) ? xr : xi;
+  const double* Y = (comp == 0 || comp == 3) ? yr : yn;
   const long long n8 = w & ~7LL;
-  double P = 0.0, Q = 0.0, R = 0.0, U = 0.0;     // xr yr, xi yi, xr yi, xi yr
-  long long k = s;
-  for (; k + 56 < n8; k += 64) {                  // 8 rows in flight
-    double2 x[8], y[8];
+  double acc = 0.0;
+  // tile t + 1's loads are in flight (registers) while the chains run over
+  // tile t (LDS)
+  constexpr int kPer = kTile / kNpThreads;
+  T xs[kPer], ys[kPer];
+  auto fetch = [&](long long tb) {
+    const int tl = n8 - tb < kTile ? (int)(n8 - tb) : kTile;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      x[j] = ldc<T>(a, ax + c0 + k + 8 * j);
-      y[j] = ldc<T>(v, c0 + k + 8 * j);
+    for (int q = 0; q < kPer; ++q) {
+      const int j = tid + q * kNpThreads;
+      const bool in = j < tl;
+      xs[q] = in ? a[ax + c0 + tb + j] : T{};
+      ys[q] = in ? v[c0 + tb + j] : T{};
     }
+  };
+#if VSIG_REFINE_KO == 2                            // tuning: no staging loads
+  if (n8 > 0) return;
+#endif
+  if (n8 > 0) fetch(0);
+  for (long long tb = 0; tb < n8; tb += kTile) {  // uniform
+    const int tl = n8 - tb < kTile ? (int)(n8 - tb) : kTile;
+    __syncthreads();                              // the previous tile is consumed
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const double yi = -y[j].y;
-      P = fma(x[j].x, y[j].x, P);
-      Q = fma(x[j].y, yi, Q);
-      R = fma(x[j].x, yi, R);
-      U = fma(x[j].y, y[j].x, U);
+    for (int q = 0; q < kPer; ++q) {
+      const int j = tid + q * kNpThreads;
+      xr[j] = (double)xs[q].x;
+      xi[j] = (double)xs[q].y;
+      yr[j] = (double)ys[q].x;
+      yn[j] = -(double)ys[q].y;
+    }
+    __syncthreads();
+    if (tb + kTile < n8) fetch(tb + kTile);
+#if VSIG_REFINE_KO != 1                            // tuning: no fma chains
+    if (tid < 32) {
+#pragma unroll 16
+      for (int k = s; k < tl; k += 8) acc = fma(X[k], Y[k], acc);
+    }
+#endif
+  }
+  if (tid < 32) {                                 // lanes 0..31 of wave 0
+    acc = acc + __shfl_xor(acc, 2, 8);
+    acc = acc + __shfl_xor(acc, 4, 8);
+    acc = acc + __shfl_xor(acc, 1, 8);            // lane 8 comp: d_comp
+    double d0 = acc;
+    const double d1 = __shfl(acc, 8), d2s = __shfl(acc, 16), d3s = __shfl(acc, 24);
+    if (tid == 0) {
+      double d1t = d1, d2 = d2s, d3 = d3s;
+      for (long long t = n8; t < w; ++t) {
+        const double2 x = ld2<T>(a, ax + c0 + t), y = ld2<T>(v, c0 + t);
+        const double yi = -y.y;
+        d0 = fma(x.x, y.x, d0);
+        d1t = fma(x.y, yi, d1t);
+        d2 = fma(x.x, yi, d2);
+        d3 = fma(y.x, x.y, d3);
+      }
+      double r = d0 - d1t;
+      const double m = d2 + d3;
+      r = fma(m, 0.0, r);
+      re = r;
+      im = m;
     }
   }
-  for (; k < n8; k += 8) {
-    const double2 x = ldc<T>(a, ax + c0 + k), y = ldc<T>(v, c0 + k);
-    const double yi = -y.y;
-    P = fma(x.x, y.x, P);
-    Q = fma(x.y, yi, Q);
-    R = fma(x.x, yi, R);
-    U = fma(x.y, y.x, U);
-  }
-  // (A0 + A1) + (A2 + A3) per ymm lane, then low + high halves
-  P = P + __shfl_xor(P, 2, 8);  Q = Q + __shfl_xor(Q, 2, 8);
-  R = R + __shfl_xor(R, 2, 8);  U = U + __shfl_xor(U, 2, 8);
-  P = P + __shfl_xor(P, 4, 8);  Q = Q + __shfl_xor(Q, 4, 8);
-  R = R + __shfl_xor(R, 4, 8);  U = U + __shfl_xor(U, 4, 8);
-  double d0 = P + __shfl_xor(P, 1, 8), d1 = Q + __shfl_xor(Q, 1, 8);
-  double d2 = R + __shfl_xor(R, 1, 8), d3 = U + __shfl_xor(U, 1, 8);
-  if (s == 0) {
-    for (long long t = n8; t < w; ++t) {
-      const double2 x = ldc<T>(a, ax + c0 + t), y = ldc<T>(v, c0 + t);
-      const double yi = -y.y;
-      d0 = fma(x.x, y.x, d0);
-      d1 = fma(x.y, yi, d1);
-      d2 = fma(x.x, yi, d2);
-      d3 = fma(y.x, x.y, d3);
-    }
-  }
-  double r = d0 - d1;
-  const double m = d2 + d3;
-  r = fma(m, 0.0, r);
-  re = r;
-  im = m;
 }
 
+// Every candidate output (entry e = u * 64 + po of unit u of an item), one
+// per block iteration: numpy's complex128 value and |c|, the max |c| by a
+// 64-bit atomic max; the last block to finish takes the lowest output index
+// attaining it (np.argmax's first-max rule) and writes the record.
 template <class T>
-__global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict__ a, const T* __restrict__ v,
-                                                            RefineGeom g, long long cap,
-                                                            RefineKeys* __restrict__ keys,
-                                                            double* __restrict__ vals,
-                                                            const long long* __restrict__ oidx,
-                                                            double2* __restrict__ cv,
-                                                            PeakPartial* __restrict__ rec,
-                                                            long long* __restrict__ items) {
-  constexpr int NW = kS2Threads / 64;
+__global__ __launch_bounds__(kNpThreads) void refine_numpy(const T* __restrict__ a, const T* __restrict__ v,
+                                                         RefineGeom g, const long long* __restrict__ items,
+                                                         long long cap, RefineKeys* __restrict__ keys,
+                                                         double* __restrict__ vals,
+                                                         long long* __restrict__ oidx,
+                                                         double2* __restrict__ cv,
+                                                         PeakPartial* __restrict__ rec) {
   const long long cnt = (long long)keys->count;
   if (keys->status || cnt == 0) return;            // uniform: no block counts itself
+#if VSIG_REFINE_KO == 3                            // tuning: the launch alone
+  return;
+#endif
   const long long n = (cnt < cap ? cnt : cap) * g.Q * 64;
-  const double lo1 = __longlong_as_double((long long)keys->max1);
-  const int tid = threadIdx.x, l = tid & 63, w = tid >> 6;
-  const int grp = l >> 3, s = l & 7;
-  __shared__ unsigned long long smask;
+  // blocks past the entry count take no part (the last-block hand-off counts
+  // only the nact blocks that have entries)
+  const long long nact = n < (long long)gridDim.x ? n : (long long)gridDim.x;
+  if ((long long)blockIdx.x >= nact) return;
+  const int tid = threadIdx.x;
+  __shared__ double tiles[4 * kTile];
   __shared__ int slast;
   __shared__ long long smin;
-  for (long long base = (long long)blockIdx.x * 64; base < n; base += (long long)gridDim.x * 64) {
-    if (w == 0) {                                  // 64 entries per block step
-      const long long e = base + l;
-      const double v1 = e < n ? vals[e] : -1.0;
-      const bool surv = v1 >= 0.0 && v1 >= lo1;
-      if (e < n && v1 >= 0.0 && !surv) vals[e] = -1.0;
-      const unsigned long long m = __ballot(surv);
-      if (l == 0) smask = m;
-      // the survivor list for the finish (items are free after stage 1)
-      unsigned long long j0 = 0;
-      if (l == 0 && m) j0 = atomicAdd(&keys->nsurv, (unsigned long long)__popcll(m));
-      j0 = __shfl(j0, 0);
-      const unsigned long long j = j0 + __popcll(m & ((1ull << l) - 1));
-      if (surv && (long long)j < cap) items[j] = e;
+  for (long long e = blockIdx.x; e < n; e += gridDim.x) {   // uniform per block
+    const long long u = e >> 6;
+    const int po = (int)(e & 63);
+    const long long o = unit_output(g, items[u / g.Q], (int)(u % g.Q), po);
+    if (o < 0) {
+      if (tid == 0) { vals[e] = -1.0; oidx[e] = -1; }
+      continue;
     }
-    __syncthreads();
-    // survivors in mask order, in batches of 8: batch b -> wave b % NW, its
-    // r-th survivor -> group r (the groups of a wave run side by side)
-    const unsigned long long mask = smask;
-    const int nsv = __popcll(mask);
-    for (int b = w; b * 8 < nsv; b += NW) {        // uniform per wave
-      const int r = b * 8 + grp;
-      if (r >= nsv) continue;                      // uniform per group
-      unsigned long long mm = mask;
-      for (int q = 0; q < r; ++q) mm &= mm - 1;
-      const int src = __builtin_ctzll(mm);
-      const long long es = base + src;
-      const long long i = g.F + oidx[es];
-      long long k0, k1;
-      tap_range(i, g.na, g.nv, k0, k1);
-      const long long nt = k1 - k0;
-      const long long ax = i - (g.nv - 1);
-      const int nch = (nt <= kBlasThreadMin || g.nthr <= 1) ? 1 : g.nthr;
-      double re = 0.0, im = 0.0;
-      long long rest = nt, c0 = k0;
-      for (int t = 0; t < nch && rest > 0; ++t) {
-        long long wd = (rest + (nch - t) - 1) / (nch - t);
-        if (wd > rest) wd = rest;
-        double pr, pi;
-        np_zdot_chunk<T>(a, v, ax, c0, wd, s, pr, pi);
-        re = re + pr;
-        im = im + pi;
-        c0 += wd;
-        rest -= wd;
-      }
-      if (s == 0) {
-        re = 0.0 + re;                             // numpy's CDOUBLE_dot sum
-        im = 0.0 + im;
-        const double av = np_cabs(re, im);
-        vals[es] = av;
-        cv[es] = make_double2(re, im);
-        atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(av));
-      }
+    const long long i = g.F + o;
+    long long k0, k1;
+    tap_range(i, g.na, g.nv, k0, k1);
+    const long long nt = k1 - k0;
+    const long long ax = i - (g.nv - 1);
+    const int nch = (nt <= kBlasThreadMin || g.nthr <= 1) ? 1 : g.nthr;
+    double re = 0.0, im = 0.0;
+    long long rest = nt, c0 = k0;
+    for (int t = 0; t < nch && rest > 0; ++t) {    // OpenBLAS threads' chunks, in order
+      long long wd = (rest + (nch - t) - 1) / (nch - t);
+      if (wd > rest) wd = rest;
+      double pr = 0.0, pi = 0.0;
+      np_zdot_chunk<T>(a, v, ax, c0, wd, tiles, pr, pi);
+      re = re + pr;
+      im = im + pi;
+      c0 += wd;
+      rest -= wd;
     }
-    __syncthreads();
+    if (tid == 0) {
+      re = 0.0 + re;                               // numpy's CDOUBLE_dot sum
+      im = 0.0 + im;
+      const double av = np_cabs(re, im);
+      vals[e] = av;
+      oidx[e] = o;
+      cv[e] = make_double2(re, im);
+      atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(av));
+    }
   }
   // the last block to finish: argmin over the entries, then the record (one
-  // release per block: the block's stores are complete at the barrier above)
+  // release per block: thread 0 made every store of this block)
   __syncthreads();
   if (tid == 0) {
     __threadfence();
-    slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)gridDim.x - 1;
+    slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
     if (slast) __threadfence();
     smin = 0x7fffffffffffffffLL;
   }
@@ -545,16 +441,10 @@ __global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict_
   const double m2 = __longlong_as_double(
       (long long)__hip_atomic_load(&keys->max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
   long long mi = 0x7fffffffffffffffLL;
-  const long long ns = (long long)__hip_atomic_load(&keys->nsurv, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-  const bool listed = ns <= cap;                   // else every entry
-  const long long ne = listed ? ns : n;
-  for (long long q = tid; q < ne; q += kS2Threads) {
-    const long long e = listed ? __hip_atomic_load(&items[q], __ATOMIC_RELAXED,
-                                                   __HIP_MEMORY_SCOPE_AGENT) : q;
-    const double ve = __hip_atomic_load(&vals[e], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (long long q = tid; q < n; q += kNpThreads) {
+    const double ve = __hip_atomic_load(&vals[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (ve == m2 && ve >= 0.0) {
-      const long long o = oidx[e];
+      const long long o = __hip_atomic_load(&oidx[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       mi = o < mi ? o : mi;
     }
   }
@@ -562,7 +452,7 @@ __global__ __launch_bounds__(kS2Threads) void refine_stage2(const T* __restrict_
     const long long om = __shfl_xor(mi, off);
     mi = om < mi ? om : mi;
   }
-  if (l == 0) atomicMin(&smin, mi);
+  if ((tid & 63) == 0) atomicMin(&smin, mi);
   __syncthreads();
   if (tid == 0 && smin != 0x7fffffffffffffffLL) {
     rec->max2 = m2;                                // numpy's |c| at its argmax
@@ -627,35 +517,21 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
     hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
                        rec, r.eps, r.cap_items, items, keys);
   }
-  // stage grids (grid-stride over the device-side candidate count): stage 1
-  // 64 / OUTS blocks per unit, stage 2 one block per 64 entries, capped so
-  // that the usual few candidates do not pay for thousands of idle blocks
-  const int split = r.cols ? 16 : 4;
-  long long units = r.cap_items * r.Q * split;
-#ifndef VSIG_REFINE_G1
-#define VSIG_REFINE_G1 256
-#define VSIG_REFINE_G2 64
+  // one output per block iteration (grid-stride over the device-side count),
+  // capped so that the usual 64 candidate outputs get a block each
+#ifndef VSIG_REFINE_GRID
+#define VSIG_REFINE_GRID 256
 #endif
-  if (units > VSIG_REFINE_G1) units = VSIG_REFINE_G1;   // one block per CU
-  const unsigned g1 = (unsigned)units;
-  long long g2l = n / 64;
-  if (g2l > VSIG_REFINE_G2) g2l = VSIG_REFINE_G2;
-  const unsigned g2 = (unsigned)g2l;
+  const long long gl = n < VSIG_REFINE_GRID ? n : VSIG_REFINE_GRID;
+  const unsigned gn = (unsigned)(gl > 0 ? gl : 1);
   auto stages = [&](auto tag) {
     using T = decltype(tag);
-    const T* a = static_cast<const T*>(r.a);
-    const T* v = static_cast<const T*>(r.v);
-    if (r.cols)
-      hipLaunchKernelGGL((refine_stage1<T, 4>), dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
-                         r.cap_items, keys, vals, oidx, cv);
-    else
-      hipLaunchKernelGGL((refine_stage1<T, 16>), dim3(g1), dim3(kS1Waves * 64), 0, st, a, v, g, items,
-                         r.cap_items, keys, vals, oidx, cv);
-    hipLaunchKernelGGL(refine_stage2<T>, dim3(g2), dim3(kS2Threads), 0, st, a, v, g, r.cap_items,
-                       keys, vals, oidx, cv, rec, items);
+    hipLaunchKernelGGL(refine_numpy<T>, dim3(gn), dim3(kNpThreads), 0, st, static_cast<const T*>(r.a),
+                       static_cast<const T*>(r.v), g, items, r.cap_items, keys, vals, oidx, cv, rec);
   };
   if (r.c128) stages(double2{});
   else stages(float2{});
+  const unsigned g2 = gn;
   if (r.out128)
     hipLaunchKernelGGL(refine_patch, dim3(g2), dim3(256), 0, st, r.cap_items, r.Q, keys, oidx, cv,
                        static_cast<double2*>(r.out128));
