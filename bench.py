@@ -220,6 +220,148 @@ def _launcher_selftest(args, world, rank, local):
     dist.destroy_process_group()
 
 
+def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
+    """Build the chain for n input samples per rank at decimation `decim`, fill
+    it on the device, run `warmup` untimed and `steps` timed steps (barrier +
+    synchronize on both sides, max over ranks) and return the elapsed time,
+    the per-stage HIP-event means and every stage against its roof."""
+    from vector_amd.shard import ChainConfig, HipBackend, StreamChain
+    from vector_amd._lib import get_context
+    granule = args.nfft * decim
+    if n % granule:
+        raise SystemExit(f"samples per GPU ({n}) must be a multiple of nfft * decim ({granule})")
+    taps, pre, tmpl = design(args.ntaps, args.template, decim)
+    ctx0 = get_context(local)
+    if args.no_refine:
+        ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, b"refine", 0), "refine")
+    cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=args.nfft, template=tmpl,
+                      freq_shift=args.freq_shift, sample_rate=args.sample_rate)
+    be = HipBackend(cfg, local)
+    chain = StreamChain(cfg, be, rank, world)
+    N = world * n
+    ny_total = N // decim
+    k0 = (ny_total // 2 + 12_345) * decim     # global input sample of the preamble
+    if args.freq_shift:   # plant the preamble so that it leaves the mixer unrotated
+        ph = 2 * np.pi * args.freq_shift * ((k0 + np.arange(len(pre))) / args.sample_rate)
+        pre = (pre * np.exp(-1j * ph)).astype(np.complex64)
+    generate_chunk(chain.x, rank * n, 20250718 + rank, pre, k0)
+    torch.cuda.synchronize()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(warmup):
+        chain.step()
+    torch.cuda.synchronize()
+    barrier()
+    lib, h = be.ctx.lib, be.ctx.h
+    lib.vsig_timing_reset(h)
+    lib.vsig_timing_enable(h, 0 if args.no_kernel_timing else 1)
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        chain.step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    barrier()
+    lib.vsig_timing_enable(h, 0)
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # per-kernel durations from HIP events on the launch stream
+    import ctypes as C
+    stages = {}
+    for name in ("fir", "psd", "xcorr", "refine"):
+        tot, cnt = C.c_double(), C.c_int64()
+        lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
+        if cnt.value:
+            stages[name] = tot.value / cnt.value
+    ny = n // decim
+    bytes_per_launch = {"fir": 8 * n + 8 * ny, "psd": 8 * ny + 4 * ny,
+                        "xcorr": 8 * (ny + chain.yhalo)}
+    m, lag, s1, s2, nout = chain.global_peak()
+    check = {"sync_lag": lag, "expected": k0 // decim, "ok": bool(lag == k0 // decim)}
+    ms_per_step = elapsed / steps * 1e3
+    yhalo = chain.yhalo
+    del chain, be
+    torch.cuda.empty_cache()
+
+    roof = None
+    kstages = {k: v for k, v in stages.items() if k in bytes_per_launch}
+    if kstages:
+        dom = max(kstages, key=lambda k: kstages[k])
+        achieved = bytes_per_launch[dom] / (kstages[dom] * 1e-3) / 1e9
+        key = f"{dom}:n={n}:ntaps={args.ntaps}:decim={decim}:nfft={args.nfft}:L={args.template}"
+        pmc = load_traffic(key)
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
+                "algorithmic_bytes": bytes_per_launch[dom],
+                "avg_launch_ms": round(kstages[dom], 4),
+                "traffic_source": pmc["source"] if pmc else None}
+        if pmc and "valu_issue_frac" in pmc:
+            roof["valu_issue_frac"] = pmc["valu_issue_frac"]
+        # the same rate against what a pure stream of this shape reached on the
+        # pool's boxes (secondary: the headline frac is against the 8 TB/s spec)
+        pc = practical_ceiling("read4to1" if (dom == "fir" and decim == 4) else "copy")
+        if pc:
+            roof["practical_peak"] = pc[0]
+            roof["practical_frac"] = round(achieved / pc[0], 4)
+            roof["practical_source"] = pc[1]
+    # every stage against its own roof: HBM bytes for all three, and for the
+    # correlator (not HBM-bound) the FP32 vector roof with the standard
+    # 5 N log2 N FFT flop count (2 FFTs + the spectrum multiply per block)
+    stage_roof = {}
+    for k, ms in kstages.items():
+        gbs = bytes_per_launch[k] / (ms * 1e-3) / 1e9
+        stage_roof[k] = {"ms": round(ms, 4), "bytes": bytes_per_launch[k], "GBs": round(gbs, 1),
+                         "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
+        pk = load_traffic(f"{k}:n={n}:ntaps={args.ntaps}:decim={decim}:nfft={args.nfft}:"
+                          f"L={args.template}")
+        if pk:
+            stage_roof[k]["traffic"] = pk["hbm_bytes_per_launch"]
+            stage_roof[k]["traffic_source"] = pk["source"]
+            if "valu_issue_frac" in pk:
+                stage_roof[k]["valu_issue_frac"] = pk["valu_issue_frac"]
+    if "xcorr" in stages:
+        M = xcorr_block(args.template)
+        L = args.template
+        hop = M - L + 1
+        if M == 16384 and hop > 1:      # the API's even hop (16-byte segment loads)
+            hop &= ~1
+        nb = -(-(ny + yhalo - L + 1) // hop)
+        flops = nb * (2 * 5 * M * np.log2(M) + 6 * M)
+        tf = flops / (stages["xcorr"] * 1e-3) / 1e12
+        stage_roof["xcorr"].update({"flops": int(flops), "TFLOPs": round(tf, 2),
+                                    "valu_peak_TFLOPs": FP32_PEAK_TF,
+                                    "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
+    if "refine" in stages:
+        stage_roof["refine"] = {"ms": round(stages["refine"], 4)}
+    # north_star's FIR+FFT target on SURVEY.md §8(d)'s unfused byte count
+    # (filter() writes y, spectrum() reads it): 8 + 8/D + 12/D B/sample
+    if "fir" in stages and "psd" in stages:
+        fp_ms = stages["fir"] + stages["psd"]
+        b = bytes_per_launch["fir"] + bytes_per_launch["psd"]
+        t = fp_ms * 1e-3
+        stage_roof["fir+psd"] = {"ms": round(fp_ms, 4), "GBs": round(b / t / 1e9, 1),
+                                 "hbm_frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
+                                 "bytes_basis": f"{b / n:.0f} B/sample (FIR 8 + 8/D, PSD 12/D)"}
+    # the whole step against the chain's algorithmic bytes (SURVEY.md §8(d):
+    # 28 B/sample at D = 1 plus the correlator's 8, 15 B/sample at D = 4)
+    chain_bytes = sum(bytes_per_launch.values())
+    stage_roof["chain"] = {"ms": round(ms_per_step, 4), "bytes_per_gpu": chain_bytes,
+                           "GBs_per_gpu": round(chain_bytes / (ms_per_step * 1e-3) / 1e9, 1),
+                           "hbm_frac": round(chain_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                           "bytes_basis": f"{chain_bytes / n:.2f} B/input sample"}
+    return {"elapsed": elapsed, "stages": stages, "stage_roof": stage_roof, "roof": roof,
+            "check": check, "taps": taps, "tmpl": tmpl}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -248,6 +390,10 @@ def main():
     ap.add_argument("--sample-rate", type=float, default=2e9, help="for --freq-shift (config 5: 2 GS/s)")
     ap.add_argument("--nchan", type=int, default=64)
     ap.add_argument("--branch-taps", type=int, default=16)
+    ap.add_argument("--no-c2-leg", action="store_true",
+                    help="skip the untimed-for-headline config-2 FIR+PSD leg after a c5 run")
+    ap.add_argument("--c2-steps", type=int, default=10)
+    ap.add_argument("--c2-samples", type=int, default=1 << 28)
     ap.add_argument("--launcher-selftest", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
@@ -270,146 +416,34 @@ def main():
         return run_pfb(args, world, rank, local, dev)
     if args.workload == "sync":
         return run_sync(args, world, rank, local, dev)
-    from vector_amd.shard import ChainConfig, HipBackend, StreamChain
-
     wdecim, wsamples, weak, wlabel = WORKLOADS[args.workload]
     decim = args.decim if args.decim is not None else wdecim
     if args.samples is not None:
         n = args.samples
     else:
         n = wsamples if weak else wsamples // world
-    granule = args.nfft * decim
-    if n % granule:
-        raise SystemExit(f"samples per GPU ({n}) must be a multiple of nfft * decim ({granule})")
-    taps, pre, tmpl = design(args.ntaps, args.template, decim)
-    from vector_amd._lib import get_context
-    ctx0 = get_context(local)
-    if args.no_refine:
-        ctx0.check(ctx0.lib.vsig_set_option(ctx0.h, b"refine", 0), "refine")
-    cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=args.nfft, template=tmpl,
-                      freq_shift=args.freq_shift, sample_rate=args.sample_rate)
-    be = HipBackend(cfg, local)
-    chain = StreamChain(cfg, be, rank, world)
+    leg = run_chain_leg(args, n, decim, rank, world, local, dev, args.steps, args.warmup)
+    elapsed, stages, stage_roof, check = leg["elapsed"], leg["stages"], leg["stage_roof"], leg["check"]
+    roof, taps, tmpl = leg["roof"], leg["taps"], leg["tmpl"]
     N = world * n
-    ny_total = N // decim
-    k0 = (ny_total // 2 + 12_345) * decim     # global input sample of the preamble
-    if args.freq_shift:   # plant the preamble so that it leaves the mixer unrotated
-        ph = 2 * np.pi * args.freq_shift * ((k0 + np.arange(len(pre))) / args.sample_rate)
-        pre = (pre * np.exp(-1j * ph)).astype(np.complex64)
-    generate_chunk(chain.x, rank * n, 20250718 + rank, pre, k0)
-    torch.cuda.synchronize()
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    for _ in range(args.warmup):
-        chain.step()
-    torch.cuda.synchronize()
-    barrier()
-    lib, h = be.ctx.lib, be.ctx.h
-    lib.vsig_timing_reset(h)
-    lib.vsig_timing_enable(h, 0 if args.no_kernel_timing else 1)
-    torch.cuda.synchronize()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        chain.step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    lib.vsig_timing_enable(h, 0)
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-
-    # per-kernel durations from HIP events on the launch stream
-    import ctypes as C
-    stages = {}
-    for name in ("fir", "psd", "xcorr", "refine"):
-        tot, cnt = C.c_double(), C.c_int64()
-        lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
-        if cnt.value:
-            stages[name] = tot.value / cnt.value
-    ny = n // decim
-    bytes_per_launch = {"fir": 8 * n + 8 * ny, "psd": 8 * ny + 4 * ny,
-                        "xcorr": 8 * (ny + chain.yhalo)}
-    m, lag, s1, s2, nout = chain.global_peak()
-    check = {"sync_lag": lag, "expected": k0 // decim, "ok": bool(lag == k0 // decim)}
-
+    # north_star's own FIR+FFT target is quoted at config 2 (2**28 samples,
+    # D = 1): after the headline's timed region, rank 0 runs that chain on its
+    # GPU as a single-rank leg (not part of `value`) and reports its stages
+    stages_c2 = None
+    if rank == 0 and args.workload == "c5" and not args.no_c2_leg and args.decim is None:
+        c2 = run_chain_leg(args, args.c2_samples, WORKLOADS["c2"][0], 0, 1, local, dev,
+                           args.c2_steps, args.warmup)
+        stages_c2 = dict(c2["stage_roof"], check=c2["check"], samples=args.c2_samples,
+                         config=(f"BASELINE configs[1]: {args.c2_samples} samples, D = 1, "
+                                 f"{args.ntaps} taps, {args.nfft}-pt PSD, {args.template}-sample "
+                                 f"xcorr (single-rank leg after the timed region)"))
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
         return
     ms_per_step = elapsed / args.steps * 1e3
     value = N / (elapsed / args.steps) / 1e6
-    roof = None
-    kstages = {k: v for k, v in stages.items() if k in bytes_per_launch}
-    if kstages:
-        dom = max(kstages, key=lambda k: kstages[k])
-        achieved = bytes_per_launch[dom] / (kstages[dom] * 1e-3) / 1e9
-        key = f"{dom}:n={n}:ntaps={args.ntaps}:decim={decim}:nfft={args.nfft}:L={args.template}"
-        pmc = load_traffic(key)
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                "algorithmic_bytes": bytes_per_launch[dom],
-                "avg_launch_ms": round(kstages[dom], 4),
-                "traffic_source": pmc["source"] if pmc else None}
-        if pmc and "valu_issue_frac" in pmc:
-            roof["valu_issue_frac"] = pmc["valu_issue_frac"]
-        # the same rate against what a pure stream of this shape reaches on the box
-        pc = practical_ceiling("read4to1" if (dom == "fir" and decim == 4) else "copy")
-        if pc:
-            roof["practical_peak"] = pc[0]
-            roof["practical_frac"] = round(achieved / pc[0], 4)
-            roof["practical_source"] = pc[1]
-    # every stage against its own roof: HBM bytes for all three, and for the
-    # correlator (not HBM-bound) the FP32 vector roof with the standard
-    # 5 N log2 N FFT flop count (2 FFTs + the spectrum multiply per block)
-    stage_roof = {}
-    for k, ms in kstages.items():
-        gbs = bytes_per_launch[k] / (ms * 1e-3) / 1e9
-        stage_roof[k] = {"ms": round(ms, 4), "bytes": bytes_per_launch[k], "GBs": round(gbs, 1),
-                         "hbm_frac": round(gbs / HBM_PEAK_GBS, 4)}
-        pk = load_traffic(f"{k}:n={n}:ntaps={args.ntaps}:decim={decim}:nfft={args.nfft}:"
-                          f"L={args.template}")
-        if pk:
-            stage_roof[k]["traffic"] = pk["hbm_bytes_per_launch"]
-            if "valu_issue_frac" in pk:
-                stage_roof[k]["valu_issue_frac"] = pk["valu_issue_frac"]
-    if "xcorr" in stages:
-        M = xcorr_block(args.template)
-        L = args.template
-        hop = M - L + 1
-        if M == 16384 and hop > 1:      # the API's even hop (16-byte segment loads)
-            hop &= ~1
-        nb = -(-(ny + chain.yhalo - L + 1) // hop)
-        flops = nb * (2 * 5 * M * np.log2(M) + 6 * M)
-        tf = flops / (stages["xcorr"] * 1e-3) / 1e12
-        stage_roof["xcorr"].update({"flops": int(flops), "TFLOPs": round(tf, 2),
-                                    "valu_peak_TFLOPs": FP32_PEAK_TF,
-                                    "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
-    if "refine" in stages:
-        stage_roof["refine"] = {"ms": round(stages["refine"], 4)}
-    # north_star's FIR+FFT target on SURVEY.md §8(d)'s unfused byte count
-    # (filter() writes y, spectrum() reads it): 8 + 8/D + 12/D B/sample
-    if "fir" in stages and "psd" in stages:
-        fp_ms = stages["fir"] + stages["psd"]
-        b = bytes_per_launch["fir"] + bytes_per_launch["psd"]
-        t = fp_ms * 1e-3
-        stage_roof["fir+psd"] = {"ms": round(fp_ms, 4), "GBs": round(b / t / 1e9, 1),
-                                 "hbm_frac": round(b / t / 1e9 / HBM_PEAK_GBS, 4),
-                                 "bytes_basis": f"{b / n:.0f} B/sample (FIR 8 + 8/D, PSD 12/D)"}
-    # the whole step against the chain's algorithmic bytes (SURVEY.md §8(d):
-    # 28 B/sample at D = 1 plus the correlator's 8, 15 B/sample at D = 4)
-    chain_bytes = sum(bytes_per_launch.values())
-    stage_roof["chain"] = {"ms": round(ms_per_step, 4), "bytes_per_gpu": chain_bytes,
-                           "GBs_per_gpu": round(chain_bytes / (ms_per_step * 1e-3) / 1e9, 1),
-                           "hbm_frac": round(chain_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-                           "bytes_basis": f"{chain_bytes / n:.2f} B/input sample"}
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         cs = args.cpu_samples or (1 << 26)
@@ -439,6 +473,7 @@ def main():
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
         "stages_roofline": stage_roof,
+        "stages_roofline_c2": stages_c2,
         "check": check,
         "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
     }

@@ -17,7 +17,8 @@ pytestmark = pytest.mark.gpu
 def test_bench_workload_small(gpu, workload):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--workload", workload,
            "--samples", str(1 << 22), "--steps", "2", "--warmup", "1",
-           "--cpu-samples", str(1 << 16), "--cpu-workers", "2"]
+           "--cpu-samples", str(1 << 16), "--cpu-workers", "2", "--c2-samples", str(1 << 21),
+           "--c2-steps", "2"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1]
@@ -32,3 +33,7 @@ def test_bench_workload_small(gpu, workload):
     assert roof["bound"] == "hbm" and 0 < roof["frac"] < 1 and roof["avg_launch_ms"] > 0
     cpu = d["cpu_baseline"]
     assert cpu["value"] > 0 and cpu["cores"] >= 1 and cpu["kind"] == "port"
+    if workload == "c5":      # north_star's config-2 FIR+PSD leg rides along
+        c2 = d["stages_roofline_c2"]
+        assert c2["check"]["ok"], c2["check"]
+        assert 0 < c2["fir+psd"]["hbm_frac"] < 1 and c2["samples"] == 1 << 21
