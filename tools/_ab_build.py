@@ -27,6 +27,12 @@ VARIANTS = {
     "libvsig_rko1": ("VSIG_REFINE_KO=1",),
     "libvsig_rko2": ("VSIG_REFINE_KO=2",),
     "libvsig_rko3": ("VSIG_REFINE_KO=3",),
+    "libvsig_konobar": ("VSIG_KO_NOBAR",),
+    "libvsig_konolds": ("VSIG_KO_NOLDS",),
+    "libvsig_koxepi": ("VSIG_KO_XEPI",),
+    "libvsig_koxsqrt": ("VSIG_KO_XSQRT",),
+    "libvsig_xw": ("VSIG_XCORR_W",),
+    "libvsig_nodskip": ("VSIG_NO_DSKIP",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

@@ -448,6 +448,9 @@ struct wave_sync_of<P, decltype(void(P::WAVE_SYNC))> { static constexpr bool val
 
 template <class P>
 __device__ __forceinline__ void plan_sync() {
+#ifdef VSIG_KO_NOBAR      // tuning knock-out (results wrong): no exchange barriers
+  return;
+#endif
   if constexpr (wave_sync_of<P>::value) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -526,10 +529,19 @@ __device__ __forceinline__ void load_rtw(float2* w, const float2* __restrict__ t
 
 template <class P>
 constexpr int nanch(int p) { return 1 + (P::R[p] - 1) / 8; }
+// anchor sets per thread in pass p: one per butterfly, or a single one when
+// every butterfly j = m(t) + b TF of the thread has the same k = j mod Ns
+// (TF a multiple of Ns, maps other than kMapIlv)
+template <class P>
+constexpr int anch_nb(int p) {
+  return (P::TF % P::ns(p) == 0 && !(p == 0 && map0_of<P>::value == kMapIlv) &&
+          !(p == P::NP - 1 && mapl_of<P>::value == kMapIlv))
+             ? 1 : P::E / P::R[p];
+}
 template <class P>
 constexpr int anch_off(int p) {
   int o = 0;
-  for (int q = 1; q < p; ++q) o += (P::E / P::R[q]) * nanch<P>(q);
+  for (int q = 1; q < p; ++q) o += anch_nb<P>(q) * nanch<P>(q);
   return o;
 }
 template <class P>
@@ -540,7 +552,7 @@ template <class P>
 __device__ __forceinline__ void load_anchors(float2* wa, const float2* __restrict__ tw, int t) {
   static_for<1, P::NP>([&](auto pi) {
     constexpr int p = decltype(pi)::value;
-    constexpr int R = P::R[p], Ns = P::ns(p), B = P::E / R, NA = nanch<P>(p);
+    constexpr int R = P::R[p], Ns = P::ns(p), B = anch_nb<P>(p), NA = nanch<P>(p);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
       const int k = bfly<P, p>(t, b) & (Ns - 1);
@@ -589,7 +601,7 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
     }
   } else {
     constexpr int NA = nanch<P>(p);
-    const float2* wa = tws.wa + anch_off<P>(p) + b * NA;
+    const float2* wa = tws.wa + anch_off<P>(p) + (anch_nb<P>(p) == 1 ? 0 : b) * NA;
     const float2 w1 = wa[0];
     float2 cur = w1;
 #if defined(VSIG_PK) && !defined(VSIG_FFT_UNPHASED)
@@ -672,6 +684,9 @@ __device__ __forceinline__ int store_base(int j) {
 
 template <class P, int p>
 __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
+#ifdef VSIG_KO_NOLDS      // tuning knock-out (results wrong): no exchange traffic
+  if constexpr (true) return;
+#endif
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
   constexpr int B = P::E / R;
@@ -689,6 +704,13 @@ __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
 
 template <class P, int p>
 __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
+#ifdef VSIG_KO_NOLDS
+  if constexpr (true) {     // keep v opaque so the passes are not folded
+#pragma unroll
+    for (int i = 0; i < P::E; ++i) asm volatile("" : "+v"(v[i].x), "+v"(v[i].y));
+    return;
+  }
+#endif
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
   if constexpr (pass_map<P, p>() == kMapIlv) {
@@ -940,6 +962,10 @@ using Plan1024q = Lanes<Partial<Plan<1024, 16, 16, 16>>, kMapPair, kMapId>;
 using Plan1024x = Lanes<Plan1024s, kMapPair, kMapPair>;
 // The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
 using Plan8192x = Swz<Plan8192>;
+// The same size on 512 threads x 16 values (four passes, the radix-2 one with
+// a single exact twiddle per thread): half the VGPRs of Plan8192x, so two
+// 512-thread correlator blocks per CU run four waves per SIMD.
+using Plan8192w = Swz<Plan<8192, 16, 16, 2, 16, 16>>;
 // The PSD's 8192-point plan with interleaved first / last passes (16-byte
 // frame loads, 8-byte |X|^2 stores, conflict-free exchanges).
 #ifndef VSIG_ILV_S            // tuning builds: the interleaved plan's padding

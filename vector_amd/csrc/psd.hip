@@ -334,6 +334,11 @@ hipError_t plan_info(int N, int* radices, int* npasses) {
     for (int q = 0; q < Plan1024s::NP; ++q) radices[q] = Plan1024s::R[q];
     return hipSuccess;
   }
+  if (N == -8192) {                 // the 512-thread 8192-point plan (correlator halves)
+    *npasses = Plan8192w::NP;
+    for (int q = 0; q < Plan8192w::NP; ++q) radices[q] = Plan8192w::R[q];
+    return hipSuccess;
+  }
   if (N == -16384) {                // the 512-thread plan (M = 32768 correlator halves)
     *npasses = Plan16384w::NP;
     for (int q = 0; q < Plan16384w::NP; ++q) radices[q] = Plan16384w::R[q];

@@ -972,7 +972,10 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     cbuf = static_cast<float2*>(x->cbuf);
   }
   const float2 *tw, *wt;
-  if ((rc = get_twiddles(c, 8192, &tw)) || (rc = get_half_tw(c, M, 512, &wt))) return rc;
+  int waves, Q, stride, plan, wstep, rsub;
+  if (vsig::xcorr_geom(M, &waves, &Q, &stride, &plan, &wstep, &rsub) != hipSuccess)
+    return fail(c, VSIG_E_UNSUPPORTED, "correlator block size");
+  if ((rc = get_twiddles(c, plan, &tw)) || (rc = get_half_tw(c, M, 512, &wt))) return rc;
   {
     Timed t(c, "xcorr");            // the whole chunked correlation + its peak pass
     for (size_t p = 0; p < x->Ps.size(); ++p) {

@@ -136,9 +136,13 @@ using PlanX32k = Plan16384w;
 using PlanX16k = Plan8192;
 #elif defined(VSIG_XCORR_ILV)
 using PlanX16k = Plan8192i;
+#elif defined(VSIG_XCORR_W)
+using PlanX16k = Plan8192w;
 #else
 using PlanX16k = Plan8192x;
 #endif
+// twiddle-table key of PlanX16k (plan_info: -8192 = Plan8192w)
+constexpr int kPlanX16kKey = std::is_same<PlanX16k, Plan8192w>::value ? -8192 : 8192;
 
 // in_index(t, e) = base(t, b) + off(e), b = e / R0: the split twiddle
 // W_M^in_index = W_M^base * W_64^half_root(e).  Plain / sigma maps: one base
@@ -263,6 +267,15 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     }
   }
   if (!partials) return;
+#ifdef VSIG_KO_XEPI       // tuning knock-out (results wrong): one sum per thread
+  {
+    float2 z = make_float2(0.f, 0.f);
+#pragma unroll
+    for (int e = 0; e < P::E; ++e) z = cadd(z, cadd(a[e], d[e]));
+    wave_partial_f(z.x, 0, z.y, 0.f, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
+    return;
+  }
+#endif
   if constexpr (KeyedRank<P>::ok) {
     // Per-thread argmax by key: the bits of |c|^2 (>= 0, so they order as the
     // floats) with the low 6 mantissa bits replaced by the output's rank in
@@ -289,7 +302,11 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
       } else {
         key = k > key ? k : key;
         any = true;
+#ifdef VSIG_KO_XSQRT      // tuning knock-out: the sum of |c| without the square roots
+        s1 += a2 * 0.5f;
+#else
         s1 += __builtin_amdgcn_sqrtf(a2);
+#endif
         s2 += a2;
       }
     };
@@ -304,9 +321,25 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
         acc(a[e], out_index<P>(t, e), KR::rank(e), IC<1>{});
       });
     }
+    // the second half's outputs i + H, i = m(t) + kStep rank(e), m(t) < kStep:
+    // an element is valid on every lane when kStep (rank + 1) <= lim - H and
+    // on none when kStep rank >= lim - H -- wave-uniform branches, so only the
+    // one straddling element of a block needs the per-lane mask (an interior
+    // block at L = 4096: the 16 lower ranks whole, the upper 16 skipped)
+    const int cut = lim - H;
     static_for<0, P::E>([&](auto ei) {
       constexpr int e = decltype(ei)::value;
-      acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
+      constexpr int c0 = KR::kStep * KR::rank(e);
+#ifdef VSIG_NO_DSKIP      // tuning builds: every element masked per lane
+      if constexpr (false) {
+#else
+      if constexpr (KR::kStep == P::TF) {      // m(t) < TF = kStep
+#endif
+        if (c0 + KR::kStep <= cut) acc(d[e], 0, KR::rank(e) + P::E, IC<0>{});
+        else if (c0 < cut) acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
+      } else {
+        acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
+      }
     });
     // lane keys (refine candidates per thread column, see xcorr_lane_keys)
     if (lkeys) lkeys[b * P::TF + tmapl<P>(t)] = key;
@@ -348,8 +381,13 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
   wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
 }
 
+// waves per SIMD: 16-value plans (Plan8192w) two 512-thread blocks per CU =
+// 4; 32-value plans two 256-thread blocks (2) or one 512-thread block (1)
+template <class P>
+constexpr int xcorr_waves_per_eu() { return P::E <= 16 ? 4 : P::TF >= 512 ? 1 : 2; }
+
 template <class P, bool PERSIST = false>
-__global__ __launch_bounds__(P::TF, P::TF >= 512 ? 1 : 2) void xcorr_half_kernel(
+__global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw,
@@ -493,7 +531,9 @@ hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* ws
     *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::N / PlanX16k::R[0];
     *wstep = 128; *rsub = 2; *plan = 8192;
   }
-  else if (M == 16384) { *waves = Plan8192::TF / 64; *Q = 2 * Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
+  else if (M == 16384) {
+    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::TF; *plan = kPlanX16kKey;
+  }
   else if (M == 8192) { *waves = Plan8192::TF / 64; *Q = Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 4096) { *waves = Plan4096::TF / 64; *Q = Plan4096::E; *stride = Plan4096::TF; *plan = 4096; }
   else return hipErrorInvalidValue;
