@@ -10,12 +10,15 @@ from oracle import ref
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("decim,L", [(1, 512), (4, 512), (2, 512), (1, 4096), (4, 4096)])
-def test_stream_chain_matches_oracle(gpu, decim, L):
-    """L = 4096 runs the bench's correlator (M = 16384, half-frame kernel)."""
+@pytest.mark.parametrize("decim,L,nfft", [(1, 512, 1024), (4, 512, 1024), (2, 512, 1024),
+                                          (1, 4096, 1024), (4, 4096, 1024), (1, 4096, 8192),
+                                          (4, 4096, 8192)])
+def test_stream_chain_matches_oracle(gpu, decim, L, nfft):
+    """L = 4096 runs the bench's correlator (M = 16384, half-frame kernel);
+    with nfft = 8192 the PSD runs inside it (vsig_xcorr_exec_psd_dev)."""
     import torch
     from vector_amd.shard import ChainConfig, HipBackend, StreamChain
-    n, nfft = 1 << 20, 1024
+    n = 1 << 20
     taps = scipy.signal.firwin(255, 0.2).astype(np.float32)
     rng = np.random.default_rng(decim)
     b = rng.integers(0, 2, size=(2, L * decim))

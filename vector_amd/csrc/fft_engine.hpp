@@ -552,7 +552,7 @@ template <class P>
 __device__ __forceinline__ void load_anchors(float2* wa, const float2* __restrict__ tw, int t) {
   static_for<1, P::NP>([&](auto pi) {
     constexpr int p = decltype(pi)::value;
-    constexpr int R = P::R[p], Ns = P::ns(p), B = anch_nb<P>(p), NA = nanch<P>(p);
+    constexpr int Ns = P::ns(p), B = anch_nb<P>(p), NA = nanch<P>(p);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
       const int k = bfly<P, p>(t, b) & (Ns - 1);

@@ -286,7 +286,11 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     // (<= 2^-17 low).  The refine band (1e-3) and its exact fp64 re-rank are
     // unaffected; with refine off the peak is the fp32 result within 8e-6.
     using KR = KeyedRank<P>;
-    const unsigned rx = rev ? 0u : 63u;
+    // rev as a compile-time flag (the uniform branch below): each key is then
+    // one v_and_or with the rank (^ 63) as an inline constant
+    auto keyed = [&](auto revc) {
+    constexpr bool kRev = decltype(revc)::value;
+    constexpr unsigned rx = kRev ? 0u : 63u;
     unsigned key = 0u;
     bool any = false;
     float s1 = 0.f, s2 = 0.f;
@@ -346,7 +350,10 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     const int rank = (int)((key & 63u) ^ rx);
     const int mi = tmapl<P>(t) + KR::kStep * rank;
     const float m = any ? __uint_as_float(key & ~63u) : -1.f;
-    wave_partial_f(m, mi, s1, s2, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
+    wave_partial_f(m, mi, s1, s2, kRev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
+    };
+    if (rev) keyed(IC<1>{});
+    else keyed(IC<0>{});
     return;
   }
   float m = -1.f, s1 = 0.f, s2 = 0.f;
