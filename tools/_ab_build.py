@@ -27,6 +27,10 @@ VARIANTS = {
     "libvsig_rko1": ("VSIG_REFINE_KO=1",),
     "libvsig_rko2": ("VSIG_REFINE_KO=2",),
     "libvsig_rko3": ("VSIG_REFINE_KO=3",),
+    "libvsig_rko4": ("VSIG_REFINE_KO=4",),
+    "libvsig_rko5": ("VSIG_REFINE_KO=5",),
+    "libvsig_rg64": ("VSIG_REFINE_GRID=64",),
+    "libvsig_rg128": ("VSIG_REFINE_GRID=128",),
     "libvsig_konobar": ("VSIG_KO_NOBAR",),
     "libvsig_konolds": ("VSIG_KO_NOLDS",),
     "libvsig_koxepi": ("VSIG_KO_XEPI",),

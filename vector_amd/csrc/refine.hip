@@ -141,6 +141,9 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     }
     block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
   }
+#if VSIG_REFINE_KO == 5                            // tuning: the first level alone
+  return;
+#endif
   if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
     __threadfence();
     slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
@@ -175,6 +178,10 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     __syncthreads();
   }
   const double t2 = sthr;
+#if VSIG_REFINE_KO == 4                            // tuning: no candidate select
+  if (tid == 0) *f.keys = RefineKeys{};
+  return;
+#endif
   for (int k = tid; k < g1; k += 256)
     if (cmax[k] >= t2) clist[atomicAdd(&ncl, 1)] = k;
   __syncthreads();
@@ -379,7 +386,7 @@ __global__ __launch_bounds__(kNpThreads) void refine_numpy(const T* __restrict__
                                                          PeakPartial* __restrict__ rec) {
   const long long cnt = (long long)keys->count;
   if (keys->status || cnt == 0) return;            // uniform: no block counts itself
-#if VSIG_REFINE_KO == 3                            // tuning: the launch alone
+#if VSIG_REFINE_KO == 3 || VSIG_REFINE_KO == 5     // tuning: the launch alone
   return;
 #endif
   const long long n = (cnt < cap ? cnt : cap) * g.Q * 64;
