@@ -29,6 +29,7 @@ VARIANTS = {
     "libvsig_rko3": ("VSIG_REFINE_KO=3",),
     "libvsig_rko4": ("VSIG_REFINE_KO=4",),
     "libvsig_rko5": ("VSIG_REFINE_KO=5",),
+    "libvsig_noxpad": ("VSIG_NO_XPAD",),
     "libvsig_rg64": ("VSIG_REFINE_GRID=64",),
     "libvsig_rg128": ("VSIG_REFINE_GRID=128",),
     "libvsig_konobar": ("VSIG_KO_NOBAR",),

@@ -1,0 +1,93 @@
+"""LDS bank-conflict model of the D = 4 FIR wave (fir_poly_kernel) (tuning aid):
+every ds op of the wave as 8-byte accesses in 4 groups of 16 lanes, bank =
+dword mod 32, extra cycles = the busiest bank's distinct dwords - 1 per group
+(MI355X_MICROARCH.md LDS table).  The model gives 96 extra cycles per wave for
+round 2's layout, exactly SQ_LDS_BANK_CONFLICT / waves of the PMC pass
+(pmc_c5_r02_v38.json: 134.2 M / 1.398 M waves); all of it in Plan256d's
+second exchange, which xpad<Plan256d, 2> (fft_engine.hpp) removes.
+  python tools/ldssim.py"""
+import itertools
+
+def conflicts(addrs_f2):       # list of 64 float2 indices (or None for inactive)
+    extra = 0
+    for g in range(4):
+        banks = {}
+        for l in range(16 * g, 16 * g + 16):
+            a = addrs_f2[l]
+            if a is None: continue
+            for dw in (2 * a, 2 * a + 1):
+                banks.setdefault(dw % 32, set()).add(dw)
+        extra += max(len(v) for v in banks.values()) - 1 if banks else 0
+    return extra
+
+def pair_map(t): return ((t & 31) << 1) | (t >> 5)
+
+def run(PADSH_F=5, PADUN_F=0, PADSH_I=4, PADUN_I=0, tqmap=lambda t: (t & 15) | ((t & 16) << 1) | ((t & 32) >> 1), verbose=False):
+    padF = lambda i: (i >> PADSH_F) << PADUN_F
+    padI = lambda i: (i >> PADSH_I) << PADUN_I
+    tot = 0; ninst = 0
+    # front Plan1024q: N=1024, E=16, R=[16,16], TF=64. pass0 store: j = pair(t), Ns=1: out r at 16 j + r
+    for r in range(16):
+        addrs = [16 * pair_map(t) + r + padF(16 * pair_map(t) + r) for t in range(64)]
+        tot += 2 * conflicts(addrs); ninst += 2   # a and d
+    # pass1 load (id map): v[r] = lds[t + 64 r]
+    for r in range(16):
+        addrs = [t + 64 * r + padF(t + 64 * r) for t in range(64)]
+        tot += 2 * conflicts(addrs); ninst += 2
+    # inverse Plan256d: N=256, E=4, R=[4,4,4,4], TF=64, thread tq
+    Ns = 1
+    for p in range(4):
+        R = 4
+        if p < 3:   # store pass p output
+            for r in range(R):
+                addrs = []
+                for t in range(64):
+                    j = tqmap(t)
+                    hi = (j // Ns) * Ns * R
+                    i = hi + (j % Ns) + r * Ns
+                    addrs.append(i + padI(i))
+                c = conflicts(addrs)
+                if verbose: print("inv store p", p, "r", r, c)
+                tot += 2 * c; ninst += 2
+        if p > 0:   # load pass p input: v[r] = lds[j + r N/R]
+            for r in range(R):
+                addrs = []
+                for t in range(64):
+                    j = tqmap(t)
+                    i = j + r * 64
+                    addrs.append(i + padI(i))
+                c = conflicts(addrs)
+                if verbose: print("inv load p", p, "r", r, c)
+                tot += 2 * c; ninst += 2
+        Ns *= R
+    return tot, ninst
+
+def run_x(xpads, tqmap):
+    tot = 0
+    Ns = 1
+    for p in range(4):
+        if p < 3:
+            S, U = xpads[p + 1]
+            for r in range(4):
+                addrs = []
+                for t in range(64):
+                    j = tqmap(t); hi = (j // Ns) * Ns * 4; i = hi + (j % Ns) + r * Ns
+                    addrs.append(i + ((i >> S) << U))
+                tot += conflicts(addrs)
+        if p > 0:
+            S, U = xpads[p]
+            for r in range(4):
+                addrs = []
+                for t in range(64):
+                    j = tqmap(t); i = j + r * 64
+                    addrs.append(i + ((i >> S) << U))
+                tot += conflicts(addrs)
+        Ns *= 4
+    return 2 * tot
+tq = lambda t: (t & 15) | ((t & 16) << 1) | ((t & 32) >> 1)
+idm = lambda t: t
+if __name__ == "__main__":
+    print("fir_poly_kernel wave, front + inverse (extra LDS cycles, LDS instructions):", run())
+    for name, m in (("poly (lanes tq)", tq), ("dec (lanes t)", idm)):
+        print(f"Plan256d inverse, {name}: 1 pad / 16 everywhere", run_x({1: (4, 0), 2: (4, 0), 3: (4, 0)}, m),
+              "| exchange 2 with 4 pads / 16", run_x({1: (4, 0), 2: (4, 2), 3: (4, 0)}, m))

@@ -365,13 +365,32 @@ struct padun_of { static constexpr int value = 0; };
 template <class P>
 struct padun_of<P, decltype(void(P::PADUN))> { static constexpr int value = P::PADUN; };
 // padding before index i: 2^PADUN float2 per 2^PADSH (PADUN = 1 keeps even
-// indices 16-byte aligned: adjacent pairs become one ds_read/write_b128)
-template <class P>
+// indices 16-byte aligned: adjacent pairs become one ds_read/write_b128).
+// Exchange X (1 <= X < NP: pass X-1's stores, pass X's loads) may pad its own
+// way (xpad, specialised per plan; X = 0: the plan's default) -- the stores
+// and loads of one exchange agree, and the LDS image of one exchange is never
+// read under another's padding.
+template <class P, int X>
+struct xpad {
+  static constexpr int S = padsh_of<P>::value;
+  static constexpr int U = padun_of<P>::value;
+};
+template <class P, int X = 0>
 __host__ __device__ constexpr int padc(int i) {
-  return (i >> padsh_of<P>::value) << padun_of<P>::value;
+  return (i >> xpad<P, X>::S) << xpad<P, X>::U;
 }
-template <class P>
-__device__ __forceinline__ int lpadp(int i) { return i + padc<P>(i); }
+template <class P, int X = 0>
+__device__ __forceinline__ int lpadp(int i) { return i + padc<P, X>(i); }
+// float2 an exchange buffer of plan P needs (the widest exchange)
+template <class P, int X = 1>
+constexpr int lds_need() {
+  if constexpr (X >= P::NP) return 0;
+  else {
+    constexpr int need = P::N + padc<P, X>(P::N - 1);
+    constexpr int rest = lds_need<P, X + 1>();
+    return need > rest ? need : rest;
+  }
+}
 template <int MAP>
 __device__ __forceinline__ int lane_map(int t) {
   if constexpr (MAP == kMapSigma) return (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1);
@@ -656,11 +675,11 @@ __device__ __forceinline__ void fft_stage(float2* v, TW tws, int t, H hook = H{}
 // lpad(base + c) for a compile-time c: multiples of 2^S become an immediate
 // offset from lpad(base) (lpad(b + 16m) = lpad(b) + 17m at S = 4), so a pass
 // needs one LDS base address per butterfly instead of one per element.
-template <class P, int C>
+template <class P, int C, int X = 0>
 __device__ __forceinline__ int lpad_off(int base, int base_pad) {
-  constexpr int S = padsh_of<P>::value;
-  if constexpr (C % (1 << S) == 0) return base_pad + C + padc<P>(C);
-  else return lpadp<P>(base + C);
+  constexpr int S = xpad<P, X>::S;
+  if constexpr (C % (1 << S) == 0) return base_pad + C + padc<P, X>(C);
+  else return lpadp<P, X>(base + C);
 }
 
 // Padded LDS index of butterfly j's output 0 in pass p, such that output r
@@ -675,11 +694,12 @@ template <class P, int p>
 __device__ __forceinline__ int store_base(int j) {
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
-  constexpr int S = padsh_of<P>::value;
+  constexpr int X = p + 1;                       // the exchange pass p stores into
+  constexpr int S = xpad<P, X>::S;
   const int hi = (j / Ns) * Ns * R;
   const int base = hi + (j & (Ns - 1));
-  if constexpr (Ns >= (1 << S)) return lpadp<P>(base);
-  else return base + padc<P>(hi);
+  if constexpr (Ns >= (1 << S)) return lpadp<P, X>(base);
+  else return base + padc<P, X>(hi);
 }
 
 template <class P, int p>
@@ -697,7 +717,7 @@ __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
       constexpr int C = r * Ns;
-      lds[bp + C + padc<P>(C)] = v[b * R + r];
+      lds[bp + C + padc<P, p + 1>(C)] = v[b * R + r];
     });
   });
 }
@@ -716,24 +736,24 @@ __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
   if constexpr (pass_map<P, p>() == kMapIlv) {
     // butterflies 2t, 2t + 1 share one padded base (never split by a pad:
     // S >= 1); with U = 1 the base is even, so each r is one 16-byte read
-    static_assert(B == 2 && (P::N / R) % (1 << padsh_of<P>::value) == 0, "interleaved pairs");
+    static_assert(B == 2 && (P::N / R) % (1 << xpad<P, p>::S) == 0, "interleaved pairs");
     const int jb = bfly<P, p>(t, 0);
-    const int jp = lpadp<P>(jb);
+    const int jp = lpadp<P, p>(jb);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
       static_for<0, R>([&](auto ri) {
         constexpr int r = decltype(ri)::value;
-        v[b * R + r] = lds[jp + b + r * (P::N / R) + padc<P>(r * (P::N / R))];
+        v[b * R + r] = lds[jp + b + r * (P::N / R) + padc<P, p>(r * (P::N / R))];
       });
     });
   } else {
     const int tl = tpass<P, p>(t);
-    const int tp = lpadp<P>(tl);
+    const int tp = lpadp<P, p>(tl);
     static_for<0, B>([&](auto bi) {
       constexpr int b = decltype(bi)::value;
       static_for<0, R>([&](auto ri) {
         constexpr int r = decltype(ri)::value;
-        v[b * R + r] = lds[lpad_off<P, b * P::TF + r * (P::N / R)>(tl, tp)];
+        v[b * R + r] = lds[lpad_off<P, b * P::TF + r * (P::N / R), p>(tl, tp)];
       });
     });
   }
@@ -754,7 +774,7 @@ __device__ __forceinline__ void fft_store_c(const float2* v, float* lds, int t) 
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
       constexpr int O = r * Ns;
-      lds[bp + O + padc<P>(O)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
+      lds[bp + O + padc<P, p + 1>(O)] = C == 0 ? v[b * R + r].x : v[b * R + r].y;
     });
   });
 }
@@ -765,12 +785,12 @@ __device__ __forceinline__ void fft_load_c(float2* v, const float* lds, int t) {
   constexpr int B = P::E / R;
   static_assert(pass_map<P, p>() != kMapIlv, "split exchange: plain maps only");
   const int tl = tpass<P, p>(t);
-  const int tp = lpadp<P>(tl);
+  const int tp = lpadp<P, p>(tl);
   static_for<0, B>([&](auto bi) {
     constexpr int b = decltype(bi)::value;
     static_for<0, R>([&](auto ri) {
       constexpr int r = decltype(ri)::value;
-      const float f = lds[lpad_off<P, b * P::TF + r * (P::N / R)>(tl, tp)];
+      const float f = lds[lpad_off<P, b * P::TF + r * (P::N / R), p>(tl, tp)];
       if constexpr (C == 0) v[b * R + r].x = f; else v[b * R + r].y = f;
     });
   });
@@ -953,6 +973,18 @@ using Plan2048s = Plan<2048, 32, 8, 32, 8>;
 // D = 2 / 4, same 64 threads): thread t holds bins t + 64 r of both.
 using Plan512d = Plan<512, 8, 8, 8, 8>;
 using Plan256d = Plan<256, 4, 4, 4, 4, 4>;
+// Plan256d's second exchange (pass 1 stores at (j / 4) 16 + j % 4 + 4 r) puts
+// 16 lanes on 4 bank pairs under 1 pad per 16 (4-way, 96 extra LDS cycles per
+// FIR wave, = SQ_LDS_BANK_CONFLICT / wave of the D = 4 FIR); 4 pads per 16
+// spread them over all 32 banks.  Exchanges 1 and 3 are conflict-free as they
+// are (tools/ldssim.py models every exchange of fir_poly_kernel / fir_dec_kernel).
+#ifndef VSIG_NO_XPAD      // tuning builds: round 2's uniform padding
+template <>
+struct xpad<Plan256d, 2> {
+  static constexpr int S = 4;
+  static constexpr int U = 2;
+};
+#endif
 // Polyphase front of the D = 4 decimating FIR: the two radix-16 passes of a
 // 1024-point transform = the 256-point spectra of its 4 polyphase components
 // (pass-1 twiddles = Plan256's table).

@@ -138,6 +138,7 @@ __global__ __launch_bounds__(P::TF) void fir_dec_kernel(
   constexpr int D = P::N / PD::N;
   static_assert(P::TF == PD::TF && P::E == D * PD::E && P::RL == P::E && PD::R[0] == PD::E,
                 "fold needs thread t to hold bins t + TF r of both plans");
+  static_assert(lds_need<PD>() <= P::LDS && lds_need<P>() <= P::LDS, "exchange buffer");
   __shared__ float2 lds[P::LDS];
   const int t = threadIdx.x;
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
@@ -232,6 +233,7 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
   constexpr int D = 4;
   static_assert(P::TF == 64 && P::E == 16 && P::NP == 2 && P::R[1] == 16 && PD::E == 4,
                 "lane layout of the reduce-scatter");
+  static_assert(lds_need<PD>() <= P::LDS && lds_need<P>() <= P::LDS, "exchange buffer");
   __shared__ float2 lds[P::LDS];
   const int t0 = threadIdx.x;
   const long long nloc = n - g0;
