@@ -4,7 +4,9 @@ dword mod 32, extra cycles = the busiest bank's distinct dwords - 1 per group
 (MI355X_MICROARCH.md LDS table).  The model gives 96 extra cycles per wave for
 round 2's layout, exactly SQ_LDS_BANK_CONFLICT / waves of the PMC pass
 (pmc_c5_r02_v38.json: 134.2 M / 1.398 M waves); all of it in Plan256d's
-second exchange, which xpad<Plan256d, 2> (fft_engine.hpp) removes.
+second exchange, which xpad<Plan256d, 2> (fft_engine.hpp) removes; likewise
+256 per D = 1 FIR wave (Plan1024x, pmc_c2_r02_v38.json: 44.6 M / 174,309 waves),
+removed by xpad<Plan1024x, 2>.
   python tools/ldssim.py"""
 import itertools
 
@@ -62,6 +64,22 @@ def run(PADSH_F=5, PADUN_F=0, PADSH_I=4, PADUN_I=0, tqmap=lambda t: (t & 15) | (
         Ns *= R
     return tot, ninst
 
+
+def plan1024x(x1, x2):
+    """One transform of the D = 1 FIR's Plan1024x (radices 16, 4, 16; pair
+    lane map in the first and last pass): extra LDS cycles with exchange 1
+    padded (S1, U1) and exchange 2 (S2, U2)."""
+    (S1, U1), (S2, U2) = x1, x2
+    p1 = lambda i: i + ((i >> S1) << U1)
+    p2 = lambda i: i + ((i >> S2) << U2)
+    tot = sum(conflicts([p1(16 * pair_map(t) + r) for t in range(64)]) for r in range(16))
+    tot += sum(conflicts([p1(t + 64 * b + 256 * r) for t in range(64)]) for b in range(4) for r in range(4))
+    tot += sum(conflicts([p2((t + 64 * b) // 16 * 64 + (t + 64 * b) % 16 + 16 * r) for t in range(64)])
+               for b in range(4) for r in range(4))
+    tot += sum(conflicts([p2(pair_map(t) + 64 * r) for t in range(64)]) for r in range(16))
+    return tot
+
+
 def run_x(xpads, tqmap):
     tot = 0
     Ns = 1
@@ -91,3 +109,6 @@ if __name__ == "__main__":
     for name, m in (("poly (lanes tq)", tq), ("dec (lanes t)", idm)):
         print(f"Plan256d inverse, {name}: 1 pad / 16 everywhere", run_x({1: (4, 0), 2: (4, 0), 3: (4, 0)}, m),
               "| exchange 2 with 4 pads / 16", run_x({1: (4, 0), 2: (4, 2), 3: (4, 0)}, m))
+    # fir_os_kernel<Plan1024x>: 4 transforms per wave (2 segments, forward + inverse)
+    print("D = 1 FIR wave (Plan1024x): 1 pad / 32 everywhere", 4 * plan1024x((5, 0), (5, 0)),
+          "| exchange 2 with 1 pad / 16", 4 * plan1024x((5, 0), (4, 0)))

@@ -992,6 +992,18 @@ using Plan1024q = Lanes<Partial<Plan<1024, 16, 16, 16>>, kMapPair, kMapId>;
 // The D = 1 FIR's one-wave overlap-save plan with the pair map in its first and
 // last pass (16-byte segment loads, conflict-free exchanges).
 using Plan1024x = Lanes<Plan1024s, kMapPair, kMapPair>;
+// Its second exchange (pass 1 stores, pass 2 pair-map loads pair(t) + 64 r)
+// puts lanes t and t + 16 of a 16-lane load group on one bank under 1 pad per
+// 32 (2-way: 256 extra LDS cycles per D = 1 FIR wave, = the c2 PMC's
+// SQ_LDS_BANK_CONFLICT / wave); 1 pad per 16 there is conflict-free for both
+// sides (tools/ldssim.py).
+#ifndef VSIG_NO_XPAD
+template <>
+struct xpad<Plan1024x, 2> {
+  static constexpr int S = 4;
+  static constexpr int U = 0;
+};
+#endif
 // The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
 using Plan8192x = Swz<Plan8192>;
 // The same size on 512 threads x 16 values (four passes, the radix-2 one with

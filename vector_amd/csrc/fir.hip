@@ -80,7 +80,7 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
     const float2* __restrict__ tw, MixArgs mix) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  __shared__ float2 lds[P::LDS];
+  __shared__ float2 lds[lds_need<P>() > P::LDS ? lds_need<P>() : P::LDS];
   const int t = threadIdx.x;
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (2 * b >= nblocks) return;  // uniform per block
