@@ -40,7 +40,11 @@ def main(src, dst, keyspec):
             if fam is None:
                 continue
             acc[fam][row["Counter_Name"]].append(float(row["Counter_Value"]))
-            meta[fam] = dict(kernel=row["Kernel_Name"].split("(")[0], vgpr=int(row["VGPR_Count"]),
+            # rocprofv3's VGPR_Count scales the descriptor's VGPR granule field by 4 on
+            # gfx950, whose granule is 8: it reads half the allocation (123 VGPRs ->
+            # 16 granules -> 64); vgpr = the allocation, vgpr_rocprof = as reported
+            meta[fam] = dict(kernel=row["Kernel_Name"].split("(")[0], vgpr=2 * int(row["VGPR_Count"]),
+                             vgpr_rocprof=int(row["VGPR_Count"]),
                              lds=int(row["LDS_Block_Size"]), scratch=int(row["Scratch_Size"]),
                              wg=int(row["Workgroup_Size"]), grid=int(row["Grid_Size"]))
     out = {"config_key_suffix": keyspec, "kernels": {}}

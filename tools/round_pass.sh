@@ -1,6 +1,9 @@
 #!/bin/bash
-# One GPU pass: GPU suite, smoke, default bench (c5 + CPU baseline), c2 bench,
-# rocprofv3 kernel stats of the default workload.  Usage: tools/round_pass.sh TAG
+# One GPU pass: GPU suite, smoke, default bench (c5 + CPU baseline + the c2
+# FIR+PSD leg), c2 / sync / pfb bench lines, rocprofv3 kernel stats of the
+# default workload; with PMC=1 also the counter passes of c5, c2 and sync
+# (tools/pmc.sh; summarise locally with tools/pmc_summary.py).
+# Usage: [PMC=1] tools/round_pass.sh TAG
 set -e
 TAG=${1:?tag}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
@@ -11,7 +14,25 @@ timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 tail -1 gpurun_out/${TAG}_smoke.txt
 timeout -k 10 400 python3 bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 cat gpurun_out/${TAG}_bench.json
-timeout -k 10 300 python3 bench.py --workload c2 --no-cpu-baseline > gpurun_out/${TAG}_c2.json 2> gpurun_out/${TAG}_c2.err
-cat gpurun_out/${TAG}_c2.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 10 --no-cpu-baseline > gpurun_out/${TAG}_prof.log 2>&1
+for w in c2 sync pfb; do
+  timeout -k 10 300 python3 bench.py --workload $w --no-cpu-baseline > gpurun_out/${TAG}_$w.json 2> gpurun_out/${TAG}_$w.err
+  cat gpurun_out/${TAG}_$w.json
+done
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/${TAG}_prof -o run -- python3 bench.py --steps 10 --no-cpu-baseline --no-c2-leg > gpurun_out/${TAG}_prof.log 2>&1
+python3 tools/db_stats.py gpurun_out/${TAG}_prof/run_results.db gpurun_out/${TAG}_kernel_stats.csv > /dev/null
+rm -rf gpurun_out/${TAG}_prof          # raw traces exceed what gpurun copies back
+echo prof done
+if [ "${PMC:-0}" = 1 ]; then
+  mkdir -p gpurun_out/${TAG}_pmcsum
+  pmc() {   # name keyspec bench-args...
+    local name=$1 key=$2; shift 2
+    bash tools/pmc.sh gpurun_out/${TAG}_pmc_$name "$@"
+    python3 tools/pmc_summary.py gpurun_out/${TAG}_pmc_$name gpurun_out/${TAG}_pmcsum/pmc_${name}_${TAG}.json "$key" > /dev/null
+    rm -rf gpurun_out/${TAG}_pmc_$name
+  }
+  pmc c5 n=2147483648:ntaps=255:decim=4:nfft=8192:L=4096 --no-c2-leg
+  pmc c2 n=268435456:ntaps=255:decim=1:nfft=8192:L=4096 --workload c2
+  pmc sync n=1073741824:L=4096 --workload sync
+  echo pmc done
+fi
 echo done
