@@ -30,6 +30,12 @@ VARIANTS = {
     "libvsig_rko4": ("VSIG_REFINE_KO=4",),
     "libvsig_rko5": ("VSIG_REFINE_KO=5",),
     "libvsig_noxpad": ("VSIG_NO_XPAD",),
+    "libvsig_nodv": ("VSIG_NO_DVSPLIT",),
+    "libvsig_nofirstd": ("VSIG_NO_FIRSTD",),
+    "libvsig_kolkey": ("VSIG_KO_LKEY",),
+    "libvsig_kopart": ("VSIG_KO_PART",),
+    "libvsig_kosums": ("VSIG_KO_SUMS",),
+    "libvsig_koxepi": ("VSIG_KO_XEPI",),
     "libvsig_rg64": ("VSIG_REFINE_GRID=64",),
     "libvsig_rg128": ("VSIG_REFINE_GRID=128",),
     "libvsig_konobar": ("VSIG_KO_NOBAR",),

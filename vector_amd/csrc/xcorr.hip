@@ -239,7 +239,12 @@ struct KeyedRank {
 // Epilogue of a half-frame block: a holds outputs i = out_index(t, e), d holds
 // i + H; a thread's indices rise through a then d (first-maximum rule as in
 // xcorr_epilogue).
-template <class P>
+// DV >= 0: the launch's interior blocks (lim == hop) keep exactly the d ranks
+// below DV (hop - H = DV kStep), a compile-time split: straight-line code with
+// no per-element branch or mask for them (the runtime split's uniform branches
+// cost ~6 % of the kernel, profiles/r03_v19_*); other blocks, and DV < 0,
+// take the runtime split.
+template <class P, int DV = -1>
 __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float2* d, long long b,
                                                     long long hop, long long nout,
                                                     float2* __restrict__ c, int store_mode,
@@ -306,14 +311,23 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
       } else {
         key = k > key ? k : key;
         any = true;
-#ifdef VSIG_KO_XSQRT      // tuning knock-out: the sum of |c| without the square roots
+#if defined(VSIG_KO_XSQRT)  // tuning knock-out: the sum of |c| without the square roots
         s1 += a2 * 0.5f;
+        s2 += a2;
+#elif defined(VSIG_KO_SUMS) // tuning knock-out: no sums at all
 #else
         s1 += __builtin_amdgcn_sqrtf(a2);
-#endif
         s2 += a2;
+#endif
       }
     };
+    if (DV >= 0 && lim == hop) {       // interior block, compile-time split
+      static_for<0, P::E>([&](auto ei) {
+        constexpr int e = decltype(ei)::value;
+        acc(a[e], 0, KR::rank(e), IC<0>{});
+        if constexpr (KR::rank(e) < DV) acc(d[e], 0, KR::rank(e) + P::E, IC<0>{});
+      });
+    } else {
     if (lim > H) {                     // every index of the a half is valid
       static_for<0, P::E>([&](auto ei) {
         constexpr int e = decltype(ei)::value;
@@ -345,11 +359,21 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
         acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
       }
     });
+    }
     // lane keys (refine candidates per thread column, see xcorr_lane_keys)
+#ifndef VSIG_KO_LKEY      // tuning knock-out (refine inputs wrong): no lane-key store
     if (lkeys) lkeys[b * P::TF + tmapl<P>(t)] = key;
+#endif
     const int rank = (int)((key & 63u) ^ rx);
     const int mi = tmapl<P>(t) + KR::kStep * rank;
     const float m = any ? __uint_as_float(key & ~63u) : -1.f;
+#ifdef VSIG_KO_PART       // tuning knock-out: one lane stores the thread's values, no wave reduction
+    if ((t & 63) == 0) {
+      PeakPartial r{(double)m, (long long)mi, (double)s1, (double)s2};
+      partials[b * (P::TF / 64) + (t >> 6)] = r;
+    }
+    return;
+#endif
     wave_partial_f(m, mi, s1, s2, kRev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
     };
     if (rev) keyed(IC<1>{});
@@ -393,7 +417,7 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
 template <class P>
 constexpr int xcorr_waves_per_eu() { return P::E <= 16 ? 4 : P::TF >= 512 ? 1 : 2; }
 
-template <class P, bool PERSIST = false>
+template <class P, bool PERSIST = false, int DV = -1>
 __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
@@ -462,7 +486,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
   });
-  xcorr_half_epilogue<P>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
+  xcorr_half_epilogue<P, DV>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
   if constexpr (!PERSIST) return;
   }
 }
@@ -485,6 +509,22 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
       return hipGetLastError();
     }
 #endif
+    // interior blocks keep the second half's ranks below (hop - H) / kStep: the
+    // common split (hop = 12288: L = 4096, 4097) has its compile-time epilogue
+    using KR = KeyedRank<PlanX16k>;
+    constexpr int kDv = PlanX16k::E / 2;
+    const long long cut = hop - PlanX16k::N;
+    const bool dv = KR::ok && KR::kStep == PlanX16k::TF && cut == (long long)kDv * KR::kStep;
+#ifdef VSIG_NO_DVSPLIT    // tuning builds: the runtime split for every block
+    if (false) {
+#else
+    if (dv) {
+#endif
+      hipLaunchKernelGGL((xcorr_half_kernel<PlanX16k, false, kDv>), dim3((unsigned)nblocks),
+                         dim3(PlanX16k::TF), 0, st, s, n, reinterpret_cast<const float4*>(Ps), off, nout,
+                         hop, c, store_mode, partials, nblocks, tw, wt, x4, lkeys);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
                        partials, nblocks, tw, wt, x4, lkeys);
