@@ -31,7 +31,6 @@ VARIANTS = {
     "libvsig_rko5": ("VSIG_REFINE_KO=5",),
     "libvsig_noxpad": ("VSIG_NO_XPAD",),
     "libvsig_nodv": ("VSIG_NO_DVSPLIT",),
-    "libvsig_nofirstd": ("VSIG_NO_FIRSTD",),
     "libvsig_kolkey": ("VSIG_KO_LKEY",),
     "libvsig_kopart": ("VSIG_KO_PART",),
     "libvsig_kosums": ("VSIG_KO_SUMS",),
