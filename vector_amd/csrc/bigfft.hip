@@ -101,7 +101,7 @@ template <class P>
 constexpr int col_frames() {
   // adjacent columns per block: <= 1024 threads, LDS <= 140 KB
   constexpr int byT = 1024 / P::TF;
-  constexpr int byL = 17920 / P::LDS;
+  constexpr int byL = 17920 / lds_size<P>();
   constexpr int f = byT < byL ? byT : byL;
   return f >= 64 ? 64 : f >= 32 ? 32 : f >= 16 ? 16 : f >= 8 ? 8 : f >= 4 ? 4 : f >= 2 ? 2 : 1;
 }
@@ -114,13 +114,13 @@ __global__ __launch_bounds__(col_frames<P>() * P::TF) void bf_col_kernel(
     BfIn in, BfOut out, float2* __restrict__ tmp, int N2, long long M,
     const float2* __restrict__ tw, const float2* __restrict__ t2, int S, int hiA) {
   constexpr int F = col_frames<P>();
-  __shared__ float2 lds[F * P::LDS];
+  __shared__ float2 lds[F * lds_size<P>()];
   const int tid = threadIdx.x;
   const int fl = tid % F, t = tid / F;
   const long long cols = N2 / F;                     // column groups per frame
   const long long f = blockIdx.x / cols;
   const int n2 = (int)(blockIdx.x % cols) * F + fl;
-  float2* lf = lds + fl * P::LDS;
+  float2* lf = lds + fl * lds_size<P>();
   float2* tf = tmp + f * M;
   float2 v[P::E];
 #pragma unroll
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(col_frames<P>() * P::TF) void bf_col_kernel(
 template <class P>
 constexpr int row_frames() {
   constexpr int byT = 1024 / P::TF;
-  constexpr int byL = 17920 / P::LDS;
+  constexpr int byL = 17920 / lds_size<P>();
   constexpr int f = byT < byL ? byT : byL;
   return f >= 8 ? 8 : f >= 4 ? 4 : f >= 2 ? 2 : 1;
 }
@@ -166,13 +166,13 @@ __global__ __launch_bounds__(row_frames<P>() * P::TF) void bf_row_kernel(
   static_assert(P::R[0] == P::RL, "in-register convolution needs a palindromic plan");
   constexpr int F = row_frames<P>();
   constexpr int N2 = P::N;
-  __shared__ float2 lds[F * P::LDS];
+  __shared__ float2 lds[F * lds_size<P>()];
   const int fl = threadIdx.x / P::TF, t = threadIdx.x % P::TF;
   const long long rows = N1 / F;
   const long long f = blockIdx.x / rows;
   const long long k1 = (blockIdx.x % rows) * F + fl;
   float2* row = tmp + f * M + k1 * N2;
-  float2* lf = lds + fl * P::LDS;
+  float2* lf = lds + fl * lds_size<P>();
   float2 v[P::E];
 #pragma unroll
   for (int e = 0; e < P::E; ++e) v[e] = row[in_index<P>(t, e)];
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(P::TF) void bf_small_kernel(BfIn in, BfOut out,
                                                          const float2* __restrict__ Bk,
                                                          const float2* __restrict__ tw) {
   static_assert(P::R[0] == P::RL, "in-register convolution needs a palindromic plan");
-  __shared__ float2 lds[P::LDS];
+  __shared__ float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   const long long f = blockIdx.x;
   float2 v[P::E];

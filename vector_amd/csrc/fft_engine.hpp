@@ -381,7 +381,8 @@ __host__ __device__ constexpr int padc(int i) {
 }
 template <class P, int X = 0>
 __device__ __forceinline__ int lpadp(int i) { return i + padc<P, X>(i); }
-// float2 an exchange buffer of plan P needs (the widest exchange)
+// float2 an exchange buffer of plan P needs (the widest exchange), and the
+// size kernels declare: P::LDS (the default padding) or more under xpad
 template <class P, int X = 1>
 constexpr int lds_need() {
   if constexpr (X >= P::NP) return 0;
@@ -391,6 +392,8 @@ constexpr int lds_need() {
     return need > rest ? need : rest;
   }
 }
+template <class P>
+constexpr int lds_size() { return lds_need<P>() > P::LDS ? lds_need<P>() : P::LDS; }
 template <int MAP>
 __device__ __forceinline__ int lane_map(int t) {
   if constexpr (MAP == kMapSigma) return (t & ~31) | ((t & 15) << 1) | ((t >> 4) & 1);

@@ -80,7 +80,7 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
     const float2* __restrict__ tw, MixArgs mix) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  __shared__ float2 lds[lds_need<P>() > P::LDS ? lds_need<P>() : P::LDS];
+  __shared__ float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (2 * b >= nblocks) return;  // uniform per block
@@ -138,8 +138,8 @@ __global__ __launch_bounds__(P::TF) void fir_dec_kernel(
   constexpr int D = P::N / PD::N;
   static_assert(P::TF == PD::TF && P::E == D * PD::E && P::RL == P::E && PD::R[0] == PD::E,
                 "fold needs thread t to hold bins t + TF r of both plans");
-  static_assert(lds_need<PD>() <= P::LDS && lds_need<P>() <= P::LDS, "exchange buffer");
-  __shared__ float2 lds[P::LDS];
+  static_assert(lds_need<PD>() <= lds_size<P>(), "exchange buffer");
+  __shared__ float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (2 * b >= nblocks) return;
@@ -233,8 +233,8 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
   constexpr int D = 4;
   static_assert(P::TF == 64 && P::E == 16 && P::NP == 2 && P::R[1] == 16 && PD::E == 4,
                 "lane layout of the reduce-scatter");
-  static_assert(lds_need<PD>() <= P::LDS && lds_need<P>() <= P::LDS, "exchange buffer");
-  __shared__ float2 lds[P::LDS];
+  static_assert(lds_need<PD>() <= lds_size<P>(), "exchange buffer");
+  __shared__ float2 lds[lds_size<P>()];
   const int t0 = threadIdx.x;
   const long long nloc = n - g0;
   const int tq0 = (t0 & 15) | ((t0 & 16) << 1) | ((t0 & 32) >> 1);

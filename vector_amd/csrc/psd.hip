@@ -33,7 +33,7 @@ __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
     const float2* __restrict__ tw, bool x4) {
   static_assert(P::TF >= 256, "one frame per block");
-  __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
+  __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   const long long u = blockIdx.x;
   float2 wa[nanch_total<P>()];
@@ -120,7 +120,7 @@ __global__ __launch_bounds__(block_threads<P>(), (P::E <= 16 ? 4 : 1)) void psd_
     const float2* __restrict__ tw) {
   constexpr int BT = block_threads<P>();
   constexpr int FPB = BT / P::TF;
-  constexpr int FL = (P::LDS + 1) / 2;
+  constexpr int FL = (lds_size<P>() + 1) / 2;
   __shared__ float2 lds[FPB * FL + tw2_size<P>()];
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
@@ -158,7 +158,7 @@ __global__ __launch_bounds__(block_threads<P>()) void spectrum_prep(
     const float2* __restrict__ u, int len, float gain, float2* __restrict__ S,
     const float2* __restrict__ tw) {
   constexpr int BT = block_threads<P>();
-  __shared__ float2 lds[(BT / P::TF) * P::LDS];
+  __shared__ float2 lds[(BT / P::TF) * lds_size<P>()];
   const int fl = threadIdx.x / P::TF;
   const int t = threadIdx.x % P::TF;
   float2 v[P::E];
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(block_threads<P>()) void spectrum_prep(
     const int i = in_index<P>(t, e);
     v[e] = (fl == 0 && i < len) ? u[i] : make_float2(0.f, 0.f);
   }
-  fft_frame<P>(v, lds + fl * P::LDS, tw, t);
+  fft_frame<P>(v, lds + fl * lds_size<P>(), tw, t);
   if (fl != 0) return;
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
@@ -185,9 +185,9 @@ template <class P, int TWL>
 __global__ __launch_bounds__(P::TF) void fft_bench_kernel(float2* __restrict__ io,
                                                                     int iters,
                                                                     const float2* __restrict__ tw) {
-  __shared__ float2 lds[P::LDS + (TWL ? tw2_size<P>() : 0)];
+  __shared__ float2 lds[lds_size<P>() + (TWL ? tw2_size<P>() : 0)];
   const int t = threadIdx.x;
-  float2* t2 = lds + P::LDS;
+  float2* t2 = lds + lds_size<P>();
   if constexpr (TWL) load_tw2<P>(t2, tw, t, P::TF);
   float2 v[P::E];
   float2* f = io + (long long)blockIdx.x * P::N;
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(P::TF) void fft_bench_kernel(float2* __restrict__ i
 template <class P, int PAIR>
 __global__ __launch_bounds__(P::TF, 2) void fft_bench_anch_kernel(float2* __restrict__ io, int iters,
                                                                   const float2* __restrict__ tw) {
-  __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
+  __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);

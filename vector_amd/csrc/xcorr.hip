@@ -80,7 +80,7 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
-  __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
+  __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   long long b = blockIdx.x;
   if (b >= nblocks) return;
@@ -427,7 +427,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
   constexpr int M = 2 * P::N;
   static_assert(P::TF % (M / 64) == 0 && (P::N / P::R[0]) % (M / 64) == 0,
                 "per-element split twiddles must be 64th roots of unity");
-  __shared__ __attribute__((aligned(16))) float2 lds[P::LDS];
+  __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
   const int t0 = threadIdx.x;
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t0);
