@@ -80,6 +80,45 @@ def plan1024x(x1, x2):
     return tot
 
 
+
+def conf_groups(addr_dw, groups, nbanks, width):
+    """Extra cycles of one ds op: per lane group, the busiest bank's distinct
+    dwords - 1 (addr_dw: first dword per lane, width dwords per lane)."""
+    extra = 0
+    for g in groups:
+        banks = {}
+        for l in g:
+            for k in range(width):
+                dw = addr_dw[l] + k
+                banks.setdefault(dw % nbanks, set()).add(dw)
+        extra += max(len(v) for v in banks.values()) - 1
+    return extra
+
+
+G8 = [list(range(8 * g, 8 * g + 8)) for g in range(8)]            # ds_write_b128
+G16 = [list(range(16 * g, 16 * g + 16)) for g in range(4)]         # ds_write_b64
+G32 = [list(range(32)), list(range(32, 64))]                       # ds_read_b64
+GR128 = [[0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27],
+         [4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31]]
+GR128 += [[l + 32 for l in g] for g in GR128]                     # ds_read_b128
+
+
+def psd8192i(x1, x2, wave=0):
+    """One frame of the PSD's Plan8192i (radices 16, 32, 16; interleaved first
+    and last pass) for wave `wave` of the 256-thread block: extra LDS cycles."""
+    (S1, U1), (S2, U2) = x1, x2
+    p1 = lambda i: i + ((i >> S1) << U1)
+    p2 = lambda i: i + ((i >> S2) << U2)
+    T = [64 * wave + l for l in range(64)]
+    tot = sum(conf_groups([2 * p1(32 * t + 16 * b + r) for t in T], G8, 32, 4)
+              for b in range(2) for r in range(0, 16, 2))
+    tot += sum(conf_groups([2 * p1(t + 256 * r) for t in T], G32, 64, 2) for r in range(32))
+    tot += sum(conf_groups([2 * p2((t // 16) * 512 + t % 16 + 16 * r) for t in T], G16, 32, 2)
+               for r in range(32))
+    tot += sum(conf_groups([2 * p2(2 * t + 512 * r) for t in T], GR128, 64, 4) for r in range(16))
+    return tot
+
+
 def run_x(xpads, tqmap):
     tot = 0
     Ns = 1
@@ -112,3 +151,6 @@ if __name__ == "__main__":
     # fir_os_kernel<Plan1024x>: 4 transforms per wave (2 segments, forward + inverse)
     print("D = 1 FIR wave (Plan1024x): 1 pad / 32 everywhere", 4 * plan1024x((5, 0), (5, 0)),
           "| exchange 2 with 1 pad / 16", 4 * plan1024x((5, 0), (4, 0)))
+    print("PSD frame, waves 0-3 (Plan8192i): 2 pads / 32 everywhere",
+          [psd8192i((5, 1), (5, 1), w) for w in range(4)],
+          "| exchange 2 with 2 pads / 64", [psd8192i((5, 1), (6, 1), w) for w in range(4)])

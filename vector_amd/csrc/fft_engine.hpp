@@ -1020,6 +1020,16 @@ using Plan8192w = Swz<Plan<8192, 16, 16, 2, 16, 16>>;
 #define VSIG_ILV_U 1
 #endif
 using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, VSIG_ILV_S, VSIG_ILV_U>;
+// Its second exchange's 16-byte pair reads (2t + 512 r: ds_read_b128 lane groups
+// of 16) meet 2-way on banks under 2 pads per 32; 2 pads per 64 spreads them
+// (tools/ldssim.py: 64 extra LDS cycles per wave and frame -> 0).
+#ifndef VSIG_NO_XPAD
+template <>
+struct xpad<Plan8192i, 2> {
+  static constexpr int S = 6;
+  static constexpr int U = 1;
+};
+#endif
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }
