@@ -31,6 +31,16 @@ VARIANTS = {
     "libvsig_rko5": ("VSIG_REFINE_KO=5",),
     "libvsig_noxpad": ("VSIG_NO_XPAD",),
     "libvsig_nodv": ("VSIG_NO_DVSPLIT",),
+    "libvsig_nosegpf": ("VSIG_NO_SEGPF",),
+    "libvsig_segpf32": ("VSIG_SEGPF_DIST=32",),
+    "libvsig_segpf128": ("VSIG_SEGPF_DIST=128",),
+    "libvsig_segpf0": ("VSIG_SEGPF_POS=0",),
+    "libvsig_segpf96": ("VSIG_SEGPF_DIST=96",),
+    "libvsig_segpf192": ("VSIG_SEGPF_DIST=192",),
+    "libvsig_segpf256": ("VSIG_SEGPF_DIST=256",),
+    "libvsig_koseg": ("VSIG_KO_SEGLD",),
+    "libvsig_kotmp": ("VSIG_KO_TMPLD",),
+    "libvsig_koboth": ("VSIG_KO_SEGLD", "VSIG_KO_TMPLD"),
     "libvsig_kolkey": ("VSIG_KO_LKEY",),
     "libvsig_kopart": ("VSIG_KO_PART",),
     "libvsig_kosums": ("VSIG_KO_SUMS",),

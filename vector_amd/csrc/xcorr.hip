@@ -446,11 +446,54 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     launder_anchors<P>(wa);
     fft_pair<P>(x, y, lds, TwAnchors{wa}, t);
   };
-  float2 a[P::E], d[P::E];
-  load_halves<P>(a, d, s, b * hop - off, n, t, x4);
-  // W_M^base: base = in_index(t, 0) (and in_index(t, R0) for the interleaved map)
+  // W_M^base: base = in_index(t, 0) (and in_index(t, R0) for the interleaved
+  // map), loaded ahead of the segment and the prefetch below (loads complete in
+  // issue order)
   const float2 w = wtz[in_index<P>(t, 0)];
   const float2 w1 = plan_ilv<P>() ? wtz[in_index<P>(t, P::R[0])] : w;
+  float2 a[P::E], d[P::E];
+#ifdef VSIG_KO_SEGLD      // tuning knock-out (results wrong): no segment loads
+  static_for<0, P::E>([&](auto ei) {
+    constexpr int e = decltype(ei)::value;
+    a[e] = make_float2((float)(t + e), (float)b);
+    d[e] = make_float2((float)(t - e), 1.f);
+  });
+#else
+  load_halves<P>(a, d, s, b * hop - off, n, t, x4);
+#endif
+  // Segment prefetch: one 4-byte load per 128-byte line of the segment kPfDist
+  // blocks ahead -- about the block that takes this slot of the XCD next
+  // (xcd_remap hands each XCD a contiguous run, two blocks per CU x 32 CUs in
+  // flight) -- so that its loads find the lines in L2 / the Infinity Cache
+  // instead of HBM.  Issued after the spectrum product (VSIG_SEGPF_POS 1; right
+  // after the segment loads with 0, where the 63-deep vmcnt makes the split
+  // step wait for them too: measured 14% slower), consumed only at the end of
+  // the block.  HBM traffic is unchanged (each line still comes from HBM once).
+  // profiles/r03_v22_xcorr_segpf_ab.txt: -5% correlator time at distance 64.
+  constexpr int kPfLines = 2 * P::N * 8 / 128 / P::TF;          // 128-byte lines per thread
+  float pfv[kPfLines];
+#pragma unroll
+  for (int k = 0; k < kPfLines; ++k) pfv[k] = 0.f;
+#ifndef VSIG_SEGPF_DIST
+#define VSIG_SEGPF_DIST 64
+#endif
+#ifndef VSIG_SEGPF_POS
+#define VSIG_SEGPF_POS 1
+#endif
+  auto prefetch = [&]() {
+#ifndef VSIG_NO_SEGPF
+    if constexpr (!PERSIST) {
+      const long long bn = b + VSIG_SEGPF_DIST;
+      const long long s0 = bn * hop - off;
+      if (bn < nblocks && s0 >= 0 && s0 + 2 * P::N <= n) {
+        const float* q = reinterpret_cast<const float*>(s + s0);
+#pragma unroll
+        for (int k = 0; k < kPfLines; ++k) pfv[k] = q[(t + k * P::TF) * 32];
+      }
+    }
+#endif
+  };
+  if constexpr (VSIG_SEGPF_POS == 0) prefetch();
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 x0 = a[e], x1 = d[e];
@@ -464,7 +507,11 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     const unsigned v0 = (unsigned)out_index<P>(t, 0) * (unsigned)sizeof(float4);
     static_for<0, P::E>([&](auto ei) {
       constexpr int e = decltype(ei)::value;
+#ifdef VSIG_KO_TMPLD      // tuning knock-out (results wrong): no template-spectrum loads
+      const float4 p = make_float4(0.5f, 0.25f, (float)e, 0.125f);
+#else
       const float4 p = buf_load4(rp, v0, out_off<P>(e) * (int)sizeof(float4));
+#endif
       a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
       d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
     });
@@ -478,6 +525,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
       d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
     }
   }
+  if constexpr (VSIG_SEGPF_POS == 1) prefetch();
   fft2(a, d);
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
@@ -487,6 +535,9 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     d[e] = csub(ev, o);
   });
   xcorr_half_epilogue<P, DV>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
+#pragma unroll
+  for (int k = 0; k < kPfLines; ++k)   // the prefetch loads stay; their values are never used
+    asm volatile("" ::"v"(pfv[k]));
   if constexpr (!PERSIST) return;
   }
 }
