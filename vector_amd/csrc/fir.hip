@@ -101,7 +101,9 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
   }
   launder_anchors<P>(wa);
+#ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+#endif
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const float2 h = Hs[out_index<P>(t, e)];
@@ -109,7 +111,9 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     d[e] = cconj(cmul(d[e], h));
   }
   launder_anchors<P>(wa);
+#ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
+#endif
   if constexpr (XS) {
     fir_store_x4<P>(a, y, b0, hop, lo, nloc, t);
     fir_store_x4<P>(d, y, b1, hop, lo, nloc, t);
