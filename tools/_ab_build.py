@@ -35,6 +35,7 @@ VARIANTS = {
     "libvsig_segpf32": ("VSIG_SEGPF_DIST=32",),
     "libvsig_segpf128": ("VSIG_SEGPF_DIST=128",),
     "libvsig_segpf0": ("VSIG_SEGPF_POS=0",),
+    "libvsig_segpf1": ("VSIG_SEGPF_POS=1",),
     "libvsig_segpf96": ("VSIG_SEGPF_DIST=96",),
     "libvsig_segpf192": ("VSIG_SEGPF_DIST=192",),
     "libvsig_segpf256": ("VSIG_SEGPF_DIST=256",),

@@ -461,15 +461,16 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
 #else
   load_halves<P>(a, d, s, b * hop - off, n, t, x4);
 #endif
-  // Segment prefetch: one 4-byte load per 128-byte line of the segment kPfDist
-  // blocks ahead -- about the block that takes this slot of the XCD next
-  // (xcd_remap hands each XCD a contiguous run, two blocks per CU x 32 CUs in
-  // flight) -- so that its loads find the lines in L2 / the Infinity Cache
-  // instead of HBM.  Issued after the spectrum product (VSIG_SEGPF_POS 1; right
-  // after the segment loads with 0, where the 63-deep vmcnt makes the split
-  // step wait for them too: measured 14% slower), consumed only at the end of
-  // the block.  HBM traffic is unchanged (each line still comes from HBM once).
-  // profiles/r03_v22_xcorr_segpf_ab.txt: -5% correlator time at distance 64.
+  // Segment prefetch: one 4-byte load per 128-byte line of the segment
+  // VSIG_SEGPF_DIST blocks ahead -- about the block that takes this slot of the
+  // XCD next (xcd_remap hands each XCD a contiguous run, two blocks per CU x 32
+  // CUs in flight) -- so that its loads find the lines in L2 instead of HBM.
+  // Issued just before the epilogue (VSIG_SEGPF_POS 2) and consumed only at
+  // the end of the block, so nothing waits for it.  Earlier issue loses: right
+  // after the segment loads (0) the 63-deep vmcnt makes the split step wait
+  // for the prefetch too (+14 %); after the spectrum product (1) the lines
+  // live long enough in the 4 MB L2 to be evicted again (+45 % L2 fills).
+  // profiles/r03_v22_xcorr_segpf_ab.txt: -5 % correlator time, +2.5 % reads.
   constexpr int kPfLines = 2 * P::N * 8 / 128 / P::TF;          // 128-byte lines per thread
   float pfv[kPfLines];
 #pragma unroll
@@ -478,7 +479,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
 #define VSIG_SEGPF_DIST 64
 #endif
 #ifndef VSIG_SEGPF_POS
-#define VSIG_SEGPF_POS 1
+#define VSIG_SEGPF_POS 2
 #endif
   auto prefetch = [&]() {
 #ifndef VSIG_NO_SEGPF
@@ -534,6 +535,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
   });
+  if constexpr (VSIG_SEGPF_POS == 2) prefetch();
   xcorr_half_epilogue<P, DV>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
 #pragma unroll
   for (int k = 0; k < kPfLines; ++k)   // the prefetch loads stay; their values are never used
