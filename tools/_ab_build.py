@@ -54,6 +54,9 @@ VARIANTS = {
     "libvsig_koxsqrt": ("VSIG_KO_XSQRT",),
     "libvsig_xw": ("VSIG_XCORR_W",),
     "libvsig_nodskip": ("VSIG_NO_DSKIP",),
+    "libvsig_fin256": ("VSIG_FIN_CHUNK=256",),
+    "libvsig_fin512": ("VSIG_FIN_CHUNK=512",),
+    "libvsig_fin1024": ("VSIG_FIN_CHUNK=1024",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

@@ -503,7 +503,10 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   PeakPartial* rec = r.rec;
   if (r.finalize) {              // the partials' finalize + select in one launch
     if (r.from_array || !r.tmp || !r.done) return hipErrorInvalidValue;
-    long long g1 = (r.nparts + 2047) / 2048;
+#ifndef VSIG_FIN_CHUNK
+#define VSIG_FIN_CHUNK 2048
+#endif
+    long long g1 = (r.nparts + VSIG_FIN_CHUNK - 1) / VSIG_FIN_CHUNK;
     if (g1 < 1) g1 = 1;
     if (g1 > kFinalizeTmp) g1 = kFinalizeTmp;
     long long chunk = (r.nparts + g1 - 1) / g1;
