@@ -504,7 +504,7 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   if (r.finalize) {              // the partials' finalize + select in one launch
     if (r.from_array || !r.tmp || !r.done) return hipErrorInvalidValue;
 #ifndef VSIG_FIN_CHUNK
-#define VSIG_FIN_CHUNK 2048
+#define VSIG_FIN_CHUNK 1024
 #endif
     long long g1 = (r.nparts + VSIG_FIN_CHUNK - 1) / VSIG_FIN_CHUNK;
     if (g1 < 1) g1 = 1;
