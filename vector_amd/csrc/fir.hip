@@ -94,8 +94,7 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     load_segment_mix<P>(a, x, g0 + b0 * hop - lo, n, t, mix);
     load_segment_mix<P>(d, x, g0 + b1 * hop - lo, n, t, mix);
   } else if constexpr (X4) {
-    load_segment_x4<P>(a, x, g0 + b0 * hop - lo, n, t);
-    load_segment_x4<P>(d, x, g0 + b1 * hop - lo, n, t);
+    load_pair_x4<P>(a, d, x, g0 + b0 * hop - lo, hop, n, t);
   } else {
     load_segment<P>(a, x, g0 + b0 * hop - lo, n, t);
     load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
@@ -259,8 +258,7 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
     load_segment_mix<P>(a, x, g0 + (2 * b) * hop - lo2, n, t, mix);
     load_segment_mix<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t, mix);
   } else if constexpr (X4) {
-    load_segment_x4<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
-    load_segment_x4<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
+    load_pair_x4<P>(a, d, x, g0 + (2 * b) * hop - lo2, hop, n, t);
   } else {
     load_segment<P>(a, x, g0 + (2 * b) * hop - lo2, n, t);
     load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);

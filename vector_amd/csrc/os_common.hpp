@@ -98,6 +98,42 @@ __device__ __forceinline__ void load_segment_x4(float2* v, const float2* __restr
   }
 }
 
+// The two segments of a one-wave FIR pair (s0 and s0 + hop) by 16-byte loads.
+// At hop = 3N/4 the second segment's first quarter is the first one's last
+// quarter in the same lanes (load i of the second = load i + 6 of the first),
+// so its rows 0..3 are copied instead of loaded: 14 loads per pair, not 16.
+template <class P>
+__device__ __forceinline__ void load_pair_x4(float2* a, float2* d, const float2* __restrict__ x,
+                                             long long s0, long long hop, long long n, int t) {
+  static_assert(map0_of<P>::value == kMapPair && P::TF == 64 && P::E == 16 && P::R[0] == 16,
+                "operand layout m(t) + 64 e");
+#ifndef VSIG_NO_PAIRLD
+  constexpr int kQ = 3 * P::N / 4;
+  if (hop == kQ && s0 >= 0 && s0 + kQ + P::N <= n) {      // uniform
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    const f4* b4 = reinterpret_cast<const f4*>(x + s0);
+    f4 u[P::E / 2 + 6];
+#pragma unroll
+    for (int i = 0; i < P::E / 2 + 6; ++i) u[i] = b4[t + 64 * i];   // float4 rows 0..13
+    auto unpack = [&](float2* v, int e, const f4& w) {
+      const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.x), __float_as_uint(w.z), false, false);
+      const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.y), __float_as_uint(w.w), false, false);
+      v[e] = make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0]));
+      v[e + 1] = make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1]));
+    };
+#pragma unroll
+    for (int i = 0; i < P::E / 2; ++i) unpack(a, 2 * i, u[i]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) d[e] = a[12 + e];
+#pragma unroll
+    for (int i = 2; i < P::E / 2; ++i) unpack(d, 2 * i, u[6 + i]);
+    return;
+  }
+#endif
+  load_segment_x4<P>(a, x, s0, n, t);
+  load_segment_x4<P>(d, x, s0 + hop, n, t);
+}
+
 // load_segment with the NCO mixer applied to each sample (global index
 // mix.i0 + s0 + i; the zero fill stays zero): one double-precision phase per
 // lane (sample g + t), then the per-element offsets' rotations

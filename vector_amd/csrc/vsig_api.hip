@@ -742,6 +742,13 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "no block size for ntaps");
   long long hop = ((long long)M - (ntaps - 1)) / decim * decim;
   if (hop < 1) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
+#ifndef VSIG_FIR1_NO_HOP768
+  // 1024-point pairs at hop 768 (ntaps 225..257): the second segment's first
+  // quarter comes from the first one's registers (load_pair_x4), 14 loads per
+  // pair instead of 16 for <= 4 % more segments (0.84 -> 0.80 ms at config 2,
+  // profiles/r03_pl1_ab.txt)
+  if (M == 1024 && decim == 1 && hop > 768 && hop < 800) hop = 768;
+#endif
   float2* hd = nullptr;
   HIPCHK(c, hipMalloc(&hd, (size_t)ntaps * sizeof(float2)));
   hipError_t e = hipMemcpyAsync(hd, taps, (size_t)ntaps * sizeof(float2), hipMemcpyHostToDevice, c->stream);
