@@ -267,14 +267,28 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
 #ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
 #endif
+#ifndef VSIG_NO_GLANE
+  // lane-major G (fir_poly_gtable): load r gives lane t its G(t, 2r), G(t, 2r + 1)
+  const float4* G4 = reinterpret_cast<const float4*>(G) + t;
+#else
   const float2* Gk = G + (t >> 4) * 256 + (t & 15);
+#endif
   float2 ua[PD::E], ud[PD::E];
 #pragma unroll
   for (int i = 0; i < PD::E; ++i) {
     float2 pa[4], pd[4];
+#ifndef VSIG_NO_GLANE
+    const float4 g01 = G4[64 * (2 * i)], g23 = G4[64 * (2 * i + 1)];
+    const float2 gq[4] = {make_float2(g01.x, g01.y), make_float2(g01.z, g01.w),
+                          make_float2(g23.x, g23.y), make_float2(g23.z, g23.w)};
+#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
+#ifndef VSIG_NO_GLANE
+      const float2 g = gq[q];
+#else
       const float2 g = Gk[16 * (4 * i + q)];
+#endif
       pa[q] = cmul(a[4 * i + q], g);
       pd[q] = cmul(d[4 * i + q], g);
     }
@@ -316,7 +330,14 @@ __global__ void fir_poly_gtable(const float2* __restrict__ Hs, float2* __restric
     re += (double)h.x * cs - (double)h.y * sn;
     im += (double)h.x * sn + (double)h.y * cs;
   }
+#ifndef VSIG_NO_GLANE
+  // lane-major: lane t = 16 k + (j & 15) uses G(t, m), m = j >> 4, from its
+  // float4 m >> 1 (fir_poly_kernel)
+  const int t = (k << 4) | (j & 15), m = j >> 4;
+  G[((m >> 1) * 64 + t) * 2 + (m & 1)] = make_float2((float)re, (float)im);
+#else
   G[i] = make_float2((float)re, (float)im);
+#endif
 }
 
 hipError_t launch_fir_poly_gtable(const float2* Hs, float2* G, hipStream_t st) {
