@@ -102,17 +102,21 @@ int vsig_synchronize(vsig_ctx* ctx);
  *                     sums of more than 10000 terms into that many chunks;
  *   "refine_eps_ppm"  the band, relative to max |c| (default 1000 = 1e-3; the
  *                     fp32 correlation error is ~1e-8 of |p| |s_segment|);
- *   "refine_cap"      most outputs revisited (default 2^20); beyond it the
+ *   "refine_cap"      0 (default): no limit -- every candidate output is
+ *                     evaluated in numpy's order however many there are (a
+ *                     flat |c|, e.g. a tone, puts every full-overlap output in
+ *                     the band; those run in refine.hip's dense form, about
+ *                     1 ms per 2^20 outputs x 4096 terms); > 0 (>= 4096): an
+ *                     explicit limit on candidate outputs -- beyond it the
  *                     record is left as the fp32 pass produced it and
  *                     vsig_refine_status reports status 1. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
 /* Outcome of the context's last refine pass (synchronises the stream):
- * status 0 refined, 1 skipped (more candidates than refine_cap), 2 no pass
- * ran (refine off, or no correlation yet); candidates = candidate items
- * (64-output thread columns of the M = 16384 / 32768 correlators, waves of the
- * M = 4096 / 8192 ones, 64-output chunks of a stored array; past the cap the
- * count stops near refine_cap / 64 items). */
+ * status 0 refined, 1 skipped (more candidate outputs than a refine_cap set
+ * > 0), 2 no pass ran (refine off, or no correlation yet); candidates =
+ * candidate items (thread columns of the M = 16384 / 32768 correlators, waves
+ * of the M = 4096 / 8192 ones, 64-output chunks of a stored array). */
 int vsig_refine_status(vsig_ctx* ctx, int32_t* status, int64_t* candidates);
 /* Hash of the kernel / ABI sources this library was built from (the Python
  * loader compares it with the sources next to it and refuses a stale build). */
@@ -219,6 +223,19 @@ int vsig_filter_channel_dev(vsig_ctx* ctx, int32_t dtype, const void* x, int64_t
  * index of the first max of |c|, the max, sum |c|, sum |c|^2. */
 int vsig_peak_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak_dev);
 int vsig_peak(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vsig_peak_t* peak);
+/* find_correlation_peak's mean_corr / std_corr (utils.py:1329-1330) exactly as
+ * numpy forms them: np.mean(np.abs(a)) and np.std(np.abs(a)) in float64, by
+ * numpy's pairwise summation over 8192-element buffers (two passes).
+ * stats_dev: device double[2] = {mean, std}.  dtype VSIG_DTYPE_C128 or
+ * VSIG_DTYPE_F64 (cross_correlate_signals' output is complex128). */
+int vsig_abs_stats_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, double* stats_dev);
+/* The same statistics of |np.correlate(a, v, mode)| without the correlation
+ * array: every output evaluated in numpy's operation order (the refine pass's
+ * dense form; O(nout x min(na, nv)) fp64 FMAs, about 1 ms per 2^20 outputs x
+ * 4096 terms) -- the exact confidence for a flat |c|, where the fused
+ * correlators' fp32 sums cannot resolve numpy's rounding-noise std. */
+int vsig_correlate_stats_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t na, const void* v,
+                             int64_t nv, int32_t mode, double* stats_dev);
 
 /* ---- stream ops either side of the chain.
  * vsig_mix_c64_dev: y[i] = x[i] * exp(j w (i0 + i) / sr) — apply_frequency_shift

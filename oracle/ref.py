@@ -204,6 +204,53 @@ def find_correlation_peak(correlation, lags, threshold_ratio=0.5):
     return lags[i], peak, conf
 
 
+def _np_pairwise(a, off, n):
+    """numpy's pairwise_sum (numpy 2.2 _core/src/umath/loops_utils.h.src) over
+    a[off:off+n] in float64: < 8 elements summed from -0.0; <= 128 with 8
+    accumulators, their fixed tree, then the tail; else split at n / 2 rounded
+    down to a multiple of 8."""
+    if n < 8:
+        r = -0.0
+        for i in range(n):
+            r += a[off + i]
+        return r
+    if n <= 128:
+        r = [a[off + j] for j in range(8)]
+        i = 8
+        while i < n - (n % 8):
+            for j in range(8):
+                r[j] += a[off + i + j]
+            i += 8
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+        while i < n:
+            res += a[off + i]
+            i += 1
+        return res
+    h = n // 2
+    h -= h % 8
+    return _np_pairwise(a, off, h) + _np_pairwise(a, off + h, n - h)
+
+
+def np_sum_order(x):
+    """np.add.reduce over a contiguous float64 array as numpy evaluates it: the
+    reduction walks buffers of 8192 elements, r = 0; r += pairwise(buffer)."""
+    a = [float(v) for v in np.asarray(x, np.float64).ravel()]
+    r = 0.0
+    for off in range(0, len(a), 8192):
+        r += _np_pairwise(a, off, min(8192, len(a) - off))
+    return r
+
+
+def np_mean_std(x):
+    """(np.mean(x), np.std(x)) of a float64 array in numpy's order: mean = sum /
+    n; std = sqrt(sum((x - mean) * (x - mean)) / n) (numpy _methods._var)."""
+    a = np.asarray(x, np.float64).ravel()
+    n = a.size
+    mean = np_sum_order(a) / n
+    d = a - mean
+    return mean, float(np.sqrt(np_sum_order(d * d) / n))
+
+
 def xcorr_peak(stream, preamble, mode="valid"):
     """Fused form used by the sync stage: correlate + find_correlation_peak.
     Returns (argmax index into the correlation, peak_lag, peak |c|, sum|c|,
@@ -411,6 +458,23 @@ def mat2wv_fields(signal, bNormalize=True):
     out[0::2] = np.real(vicData).astype(np.int16)
     out[1::2] = np.imag(vicData).astype(np.int16)
     return out, fRMSdBfs, fPeakPowerdBfs
+
+
+def generate_sample_packet(duration, sr, frequency, amplitude=1.0):
+    """utils.py:679-686: a complex128 tone of int(sr * duration) samples."""
+    t = np.linspace(0, duration, int(sr * duration), endpoint=False)
+    return amplitude * np.exp(2j * np.pi * frequency * t)
+
+
+def periodic_vector(packet, period_samples, total_samples, start=0):
+    """unified_gui.py:1712, 1755-1769: a complex64 vector of total_samples with
+    the packet added every period_samples from start, while it fits."""
+    vector = np.zeros(total_samples, dtype=np.complex64)
+    pos = start
+    while pos + len(packet) <= total_samples:
+        vector[pos:pos + len(packet)] += packet
+        pos += period_samples
+    return vector
 
 
 # ---------------------------------------------------------------------------

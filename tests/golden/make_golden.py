@@ -28,6 +28,10 @@ Fixture inventory (SURVEY.md §8(c) golden set G1-G5):
                        vector (full mode) and, for packets 1 and 3, in their own packet and
                        find_packet_location_in_vector (utils.py:1258-1342, 1372-1434) --
                        near-tie argmaxes (top-2 |c| gaps 1e-13 .. 7e-12 relative)
+  refine_flat.npz      flat |c| (every full-overlap output an exact tie): a 2^21-sample
+                       tone against its first 4096 samples, 30 periods of
+                       data/packet_1.mat in a vector, a tone template over a tone
+                       ('valid', numpy's confidence from a rounding-noise std)
   stream_ops.npz       apply_frequency_shift (utils.py:120-127), transplant_packet_in_vector
                        (utils.py:1437-1501), resample_signal (utils.py:107-118)
   wv.npz               mat2wv's SMU-WV file bytes (vector_analyzer/mat_to_wv_converter.py:7-64)
@@ -278,6 +282,62 @@ def gen_tone_transplant():
     save("tone_transplant.npz", **out)
 
 
+def gen_refine_flat():
+    """Flat |c| on the reference's own kind of data, where every full-overlap
+    output ties with the maximum up to numpy's rounding (np.argmax's pick and
+    np.std are decided by the rounding of numpy's own sums):
+      (a) a 2^21-sample tone (generate_sample_packet, utils.py:679-686) against
+          its first 4096 samples, 'full' (cross_correlate_signals +
+          find_correlation_peak, utils.py:1258-1342); the tone is regenerated
+          by the tests (oracle.ref.generate_sample_packet) and checked against
+          the sha256 stored here;
+      (b) 30 instances of data/packet_1.mat (load_packet_info, complex64) in
+          a vector built as unified_gui.py:1712, 1755-1769 does (period 56000
+          samples), against seg1 = the .mat packet's first 4096 samples
+          (complex128), and find_packet_location_in_vector;
+      (c) a 1000-sample tone template over a 20000-sample tone, 'valid': every
+          output in the band, numpy's std = rounding noise (confidence > 0)."""
+    import hashlib
+    from oracle.ref import periodic_vector
+    out = {}
+    # (a)
+    dur, sr, f = 1.0, float(2 ** 21), 40_961.5
+    tone = refutils.generate_sample_packet(dur, sr, f)
+    seg = refutils.extract_reference_segment(tone, 0, 4096)
+    c, lags = refutils.cross_correlate_signals(seg, tone)
+    lag, val, conf = refutils.find_correlation_peak(c, lags)
+    a = np.abs(c)
+    out.update(a_args=np.array([dur, sr, f]), a_sha=np.array(hashlib.sha256(tone.tobytes()).hexdigest()),
+               a_peak=np.array([lag, val, conf], np.float64), a_argmax=np.int64(np.argmax(a)),
+               a_nearmax=np.int64(np.count_nonzero(a >= a.max() * (1 - 1e-12))),
+               a_stats=np.array([a.mean(), a.std()]))
+    del c, a
+    # (b)
+    y, _pre = refutils.load_packet_info(os.path.join(REF, "data", "packet_1.mat"))
+    pk = np.asarray(sio.loadmat(os.path.join(REF, "data", "packet_1.mat"))["Y"]).ravel()
+    seg1 = refutils.extract_reference_segment(pk, 0, 4096)
+    period, reps = 56_000, 30
+    vec = periodic_vector(y, period, period * (reps - 1) + len(y))
+    c, lags = refutils.cross_correlate_signals(seg1, vec)
+    lag, val, conf = refutils.find_correlation_peak(c, lags)
+    a = np.abs(c)
+    out.update(b_args=np.array([period, reps, period * (reps - 1) + len(y)]),
+               b_sha=np.array(hashlib.sha256(vec.tobytes()).hexdigest()),
+               b_peak=np.array([lag, val, conf], np.float64), b_argmax=np.int64(np.argmax(a)),
+               b_nearmax=np.int64(np.count_nonzero(a >= a.max() * (1 - 1e-12))),
+               b_loc=np.array(refutils.find_packet_location_in_vector(vec, pk, seg1), np.float64))
+    del c, a
+    # (c)
+    tone = refutils.generate_sample_packet(0.02, 1e6, 12_345.0)
+    tm = refutils.extract_reference_segment(tone, 0, 1000)
+    c, lags = refutils.cross_correlate_signals(tm, tone, mode="valid")
+    lag, val, conf = refutils.find_correlation_peak(c, lags)
+    a = np.abs(c)
+    out.update(c_tone=tone, c_peak=np.array([lag, val, conf], np.float64),
+               c_stats=np.array([a.mean(), a.std()]), c_abs=a)
+    save("refine_flat.npz", **out)
+
+
 def gen_stream_ops():
     import contextlib
     import io
@@ -360,6 +420,7 @@ if __name__ == "__main__":
             globals()[f"gen_{name}"]()
         sys.exit(0)
     gen_tone_transplant()
+    gen_refine_flat()
     gen_stream_ops()
     gen_wv()
     gen_channel()

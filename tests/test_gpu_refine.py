@@ -155,19 +155,22 @@ def test_streaming_correlator_refined(gpu):
     assert peak == want[2]
 
 
-def test_refine_cap_and_off(gpu):
-    """Flat |c| beyond the cap: the record stays the fp32 one, the status says
-    so and the numpy front end warns; refine off: no pass at all."""
+def test_refine_cap_opt_in_and_off(gpu):
+    """Default: no cap (every candidate evaluated, status 0).  An explicit
+    'refine_cap' below the candidate count leaves the record fp32 (status 1, the
+    numpy front end warns); refine off: no pass at all."""
     import ctypes as C
     ctx = gpu.get_context()
     tone = np.exp(2j * np.pi * 0.01 * np.arange(300_000)).astype(np.complex64)
+    gpu.correlate_peak(tone[:1000], tone, "valid")
+    assert _status(gpu)[0] == 0
     ctx.check(ctx.lib.vsig_set_option(ctx.h, b"refine_cap", 8192), "cap")
     try:
         with pytest.warns(RuntimeWarning, match="refine_cap"):
             gpu.correlate_peak(tone[:1000], tone, "valid")
         assert _status(gpu)[0] == 1
     finally:
-        ctx.check(ctx.lib.vsig_set_option(ctx.h, b"refine_cap", 1 << 20), "cap")
+        ctx.check(ctx.lib.vsig_set_option(ctx.h, b"refine_cap", 0), "cap")
     ctx.check(ctx.lib.vsig_set_option(ctx.h, b"refine", 0), "off")
     try:
         gpu.correlate_peak(tone[:1000], tone[:5000], "valid")
@@ -177,6 +180,102 @@ def test_refine_cap_and_off(gpu):
     v = C.c_int()
     ctx.check(ctx.lib.vsig_get_option(ctx.h, b"refine", C.byref(v)), "get")
     assert v.value == 1
+    ctx.check(ctx.lib.vsig_get_option(ctx.h, b"refine_cap", C.byref(v)), "get")
+    assert v.value == 0
+
+
+def _flat_tone(g):
+    dur, sr, f = g["a_args"]
+    tone = ref.generate_sample_packet(float(dur), float(sr), float(f))
+    import hashlib
+    assert hashlib.sha256(tone.tobytes()).hexdigest() == str(g["a_sha"]), \
+        "numpy regenerated a different tone than the golden's"
+    return tone
+
+
+def test_flat_tone_2e21_exact(gpu):
+    """The reference's flat case at scale (refine_flat.npz (a), made by the
+    reference's cross_correlate_signals + find_correlation_peak): a 2^21-sample
+    tone against its first 4096 samples, 'full' -- 2 093 057 outputs within
+    1e-12 of the max, every full-overlap output in the refine band.  numpy's
+    argmax (decided by the rounding of its own sums) and |c| exactly, fused and
+    through the stored complex128 array."""
+    g = golden("refine_flat.npz")
+    tone = _flat_tone(g)
+    seg = tone[:4096]
+    want_lag, want_val, want_conf = g["a_peak"]
+    lag, val, conf = gpu.correlate_peak(seg, tone)
+    st, cand = _status(gpu)
+    print(f"2^21 tone: {cand} candidate items, lag {int(lag)} (numpy {int(want_lag)})")
+    assert st == 0
+    assert lag == want_lag
+    assert val == want_val
+    assert conf == pytest.approx(want_conf, rel=1e-4, abs=1e-7)
+    c, lags = gpu.cross_correlate_signals(seg, tone)
+    assert int(np.argmax(np.abs(c))) == int(g["a_argmax"])
+    lag2, val2, conf2 = gpu.find_correlation_peak(c, lags)
+    assert (lag2, val2) == (want_lag, want_val)
+    assert conf2 == pytest.approx(want_conf, rel=1e-4, abs=1e-7)
+
+
+def test_periodic_tone_packet_vector_exact(gpu):
+    """refine_flat.npz (b): 30 instances of the reference's data/packet_1.mat in a
+    vector built as the reference's GUI builds it (unified_gui.py:1712,
+    1755-1769), searched with the packet's first 4096 samples: numpy's lag, |c|
+    and find_packet_location_in_vector result exactly."""
+    g = golden("refine_flat.npz")
+    t = golden("tone_transplant.npz")
+    period, reps, total = (int(v) for v in g["b_args"])
+    pk, seg = t["packet1"], t["seg1"]
+    vec = ref.periodic_vector(pk.astype(np.complex64), period, total)
+    import hashlib
+    assert hashlib.sha256(vec.tobytes()).hexdigest() == str(g["b_sha"])
+    want_lag, want_val, want_conf = g["b_peak"]
+    lag, val, conf = gpu.correlate_peak(seg, vec)
+    assert _status(gpu)[0] == 0
+    assert lag == want_lag
+    assert val == want_val
+    assert conf == pytest.approx(want_conf, rel=1e-4, abs=1e-7)
+    c, lags = gpu.cross_correlate_signals(seg, vec)
+    assert int(np.argmax(np.abs(c))) == int(g["b_argmax"])
+    loc = gpu.find_packet_location_in_vector(vec, pk, seg)
+    want = g["b_loc"]
+    assert loc[0] == want[0] and loc[1] == want[1]
+    assert loc[2] == pytest.approx(want[2], rel=1e-4, abs=1e-7)
+
+
+def test_flat_valid_confidence_exact(gpu):
+    """refine_flat.npz (c): a 1000-sample tone template over a 20000-sample tone,
+    'valid' -- |c| is flat, numpy's std_corr (1.07e-13) is rounding noise and
+    its confidence 0.318 follows from it.  Fused: the fp32 sums cannot resolve
+    that std, so every output is re-evaluated in numpy's order and numpy's
+    two-pass statistics are formed from them (vsig_correlate_stats_dev); from
+    the stored array: vsig_abs_stats_dev.  Both equal numpy's to the bit."""
+    g = golden("refine_flat.npz")
+    tone = g["c_tone"]
+    tm = tone[:1000]
+    want_lag, want_val, want_conf = g["c_peak"]
+    lag, val, conf = gpu.correlate_peak(tm, tone, "valid")
+    assert (lag, val) == (want_lag, want_val)
+    assert conf == want_conf
+    c, lags = gpu.cross_correlate_signals(tm, tone, "valid")
+    assert np.array_equal(np.abs(c), g["c_abs"])         # every output numpy's (dense refine)
+    assert gpu.find_correlation_peak(c, lags) == (want_lag, want_val, want_conf)
+
+
+@pytest.mark.parametrize("n", [1, 7, 100, 8192, 8193, 50_000, (1 << 20) + 3])
+def test_abs_stats_numpy_order(gpu, n):
+    """vsig_abs_stats_dev = np.mean(np.abs(a)), np.std(np.abs(a)) bit for bit
+    (complex128 and float64)."""
+    import torch
+    rng = np.random.default_rng(n)
+    a = (rng.standard_normal(n) + 1j * rng.standard_normal(n)) * 10 ** rng.uniform(-3, 3, n)
+    ctx = gpu.get_context()
+    for arr, code in ((a, "c128"), (a.real.copy(), "f64")):
+        t = torch.from_numpy(arr).cuda()
+        m, sd = gpu.dsp._abs_stats(t, code, ctx)
+        assert m == np.mean(np.abs(arr))
+        assert sd == np.std(np.abs(arr))
 
 
 @pytest.mark.parametrize("L,ns,mode", [(10_000, 60_000, "valid"), (20_000, 90_000, "full"),
@@ -250,26 +349,30 @@ def test_near_tie_columns_every_plan(gpu, L, ratio, swapped):
     assert _status(gpu)[0] == 0
 
 
-def test_flat_correlation_over_cap_is_cheap(gpu):
-    """A tone against itself over 2^24 samples (M = 16384, 5461 blocks, three
-    finalize chunks): every thread column is in the band, far past the default
-    cap of 2^20 outputs; the fused finalize stops appending at the cap, the
-    record stays the fp32 one (status 1) and the pass costs milliseconds."""
+def test_flat_correlation_2e24_dense(gpu):
+    """A tone against itself over 2^24 samples, 'valid' (M = 16384, 5461 blocks):
+    every one of the 2^24 - 4095 outputs is a candidate.  No cap: the dense form
+    evaluates all of them in numpy's order (status 0); the record's |c| is
+    numpy's value at the returned lag (oracle/npdot.c), and the pass costs
+    milliseconds (numpy: about half a minute)."""
     import time
+    import torch
+    from oracle import npdot
     n, L = 1 << 24, 4096
     ph = 2 * np.pi * 0.01 * np.arange(n)
     tone = torch.polar(torch.ones(n, dtype=torch.float64),
                        torch.from_numpy(ph)).to(torch.complex64).cuda()
     tmpl = tone[:L].cpu().numpy()
-    with pytest.warns(RuntimeWarning, match="refine_cap"):
-        gpu.correlate_peak(tmpl, tone, "valid")      # warm-up (plans, scratch)
+    gpu.correlate_peak(tmpl, tone, "valid")           # warm-up (plans, scratch)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    with pytest.warns(RuntimeWarning, match="refine_cap"):
-        lag, val, _ = gpu.correlate_peak(tmpl, tone, "valid")
+    lag, val, _ = gpu.correlate_peak(tmpl, tone, "valid")
     dt = time.perf_counter() - t0
     st, cand = _status(gpu)
-    assert st == 1 and cand > (1 << 20) // 64
+    print(f"2^24 flat: {cand} candidate items, {dt * 1e3:.1f} ms")
+    assert st == 0 and cand > (1 << 20) // 64
     assert 0 <= lag < n - L + 1
-    assert val == pytest.approx(L, rel=1e-4)         # |c| = L everywhere
+    seg = tone[int(lag):int(lag) + L].cpu().numpy().astype(np.complex128)
+    want = npdot.cabs(np.array([npdot.zdotu(seg, np.conj(tmpl.astype(np.complex128)), 1)]))[0]
+    assert val == want
     assert dt < 0.5

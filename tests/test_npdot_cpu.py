@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 
 from conftest import golden
-from oracle import npdot
+from oracle import npdot, ref
 from vector_amd._lib import numpy_blas_threads
 
 T = numpy_blas_threads()
@@ -66,3 +66,26 @@ def test_tone_self_ties_decided_by_the_order(i):
     assert int(np.argmax(a)) == int(g[f"pkt{i}_argmax"])
     assert a.max() == g[f"pkt{i}_peak"][1]
     assert np.array_equal(_bits(c), _bits(np.correlate(pk, seg, "full")))
+
+
+@pytest.mark.parametrize("n", [1, 5, 7, 8, 9, 100, 127, 128, 129, 255, 256, 1000, 8191, 8192,
+                               8193, 16_385, 20_000, 65_537, 100_003])
+def test_np_sum_order_and_mean_std(n):
+    """numpy's float64 reduction order (oracle.ref.np_sum_order: pairwise sums
+    over 8192-element buffers) and np.mean / np.std built on it, bit for bit --
+    what reduce.hip np_stats evaluates for find_correlation_peak's confidence
+    (utils.py:1329-1330)."""
+    rng = np.random.default_rng(n)
+    x = np.abs(rng.standard_normal(n) + 1j * rng.standard_normal(n)) * 10 ** rng.uniform(-2, 2, n)
+    assert ref.np_sum_order(x) == np.sum(x)
+    m, sd = ref.np_mean_std(x)
+    assert m == np.mean(x)
+    assert sd == np.std(x)
+
+
+def test_np_mean_std_flat_golden():
+    """The reference's flat |c| (refine_flat.npz (c): a tone template over a
+    tone, 'valid'): numpy's std is rounding noise, reproduced exactly."""
+    g = golden("refine_flat.npz")
+    m, sd = ref.np_mean_std(g["c_abs"])
+    assert (m, sd) == tuple(g["c_stats"])

@@ -89,6 +89,8 @@ SIGNATURES = {
     "vsig_filter_channel_dev": (C.c_int, [P, I32, P, I64, C.c_double, C.c_double, C.c_double, P]),
     "vsig_peak_dev": (C.c_int, [P, I32, P, I64, P]),
     "vsig_peak": (C.c_int, [P, I32, P, I64, P]),
+    "vsig_abs_stats_dev": (C.c_int, [P, I32, P, I64, P]),
+    "vsig_correlate_stats_dev": (C.c_int, [P, I32, P, I64, P, I64, I32, P]),
     "vsig_mix_c64_dev": (C.c_int, [P, P, I64, C.c_double, C.c_double, I64, P]),
     "vsig_scale_c64_dev": (C.c_int, [P, P, I64, C.c_float, P]),
     "vsig_wv_quantize_dev": (C.c_int, [P, P, I64, C.c_float, P]),
@@ -153,12 +155,28 @@ def load_library(path: str | None = None):
         return lib
 
 
+_warned_no_threadpoolctl = False
+
+
 def numpy_blas_threads() -> int:
     """The thread count of the OpenBLAS behind this process's numpy (its zdotu
     splits a complex128 dot of more than 10000 terms into that many chunks,
-    which decides the rounding of np.correlate's long sums); 1 if unknown."""
+    which decides the rounding of np.correlate's long sums); read at every call
+    (threadpool_limits / OPENBLAS_NUM_THREADS may change it).  1 if unknown --
+    with a warning when threadpoolctl is missing: correlations with more than
+    10000 overlap terms then match numpy only if its OpenBLAS runs one thread."""
+    global _warned_no_threadpoolctl
     try:
         from threadpoolctl import threadpool_info
+    except ImportError:
+        if not _warned_no_threadpoolctl:
+            import warnings
+            warnings.warn("threadpoolctl is not importable: numpy's OpenBLAS thread count is "
+                          "taken as 1 for the exact argmax of correlations over 10000 terms",
+                          RuntimeWarning, stacklevel=2)
+            _warned_no_threadpoolctl = True
+        return 1
+    try:
         for d in threadpool_info():
             if d.get("internal_api") == "openblas":
                 return max(1, min(1024, int(d.get("num_threads", 1))))
@@ -178,9 +196,17 @@ class Context:
             raise VsigUnavailable(f"vsig_init(device={device}) failed: "
                                   f"{lib.vsig_errstr(rc).decode()}")
         self.lib, self.h, self.device = lib, h, device
-        # the refine matches numpy's complex128 sums operation for operation;
-        # OpenBLAS splits those over 10000 terms across its threads
-        self.check(lib.vsig_set_option(h, b"blas_threads", numpy_blas_threads()), "blas_threads")
+        self.blas_threads = None
+        self.sync_blas_threads()
+
+    def sync_blas_threads(self):
+        """The refine matches numpy's complex128 sums operation for operation;
+        OpenBLAS splits those over 10000 terms across its threads: hand the
+        library numpy's current thread count (called before each correlation)."""
+        t = numpy_blas_threads()
+        if t != self.blas_threads:
+            self.check(self.lib.vsig_set_option(self.h, b"blas_threads", t), "blas_threads")
+            self.blas_threads = t
 
     def check(self, rc: int, what: str):
         if rc != VSIG_OK:

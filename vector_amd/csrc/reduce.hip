@@ -103,4 +103,172 @@ hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, i
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// numpy's float64 statistics of |a| (find_correlation_peak's mean_corr /
+// std_corr, utils.py:1329-1330, over np.abs(correlation)):
+//   sum  = np.add.reduce over a contiguous array: numpy's reduction walks the
+//          array in buffers of 8192 elements, r = 0; r += pairwise(buffer),
+//          pairwise = numpy's pairwise_sum (umath loops_utils.h.src: blocks of
+//          <= 128 summed with 8 accumulators and a fixed tree, larger ranges
+//          split at n / 2 rounded down to a multiple of 8; fewer than 8
+//          elements summed from -0.0);
+//   mean = sum / n;  std = sqrt(sum((|a| - mean) * (|a| - mean)) / n)
+//          (np.std's _var: x = arr - arrmean, x = x * x, the same sum).
+// Pinned against numpy by tests/test_npdot_cpu.py (oracle/npdot.c np_stats).
+// One wave per buffer: lane-parallel leaves (each stored at its offset / 32:
+// leaves hold >= 57 elements, so at most one starts in any 32-element
+// window), then lane 0 combines them in the pairwise tree's order; one block
+// adds the buffer sums in order.
+// ---------------------------------------------------------------------------
+#pragma clang fp contract(off)
+
+constexpr int kNpBuf = 8192;
+
+template <class T>
+__device__ __forceinline__ double np_elem(const T* __restrict__ a, long long i, int sq, double mean) {
+  double x = absval<T>(a, i);
+  if (sq) {
+    x = x - mean;
+    x = x * x;
+  }
+  return x;
+}
+
+template <class T>
+__device__ double np_leaf(const T* __restrict__ a, long long off, int n, int sq, double mean) {
+  if (n < 8) {
+    double res = -0.0;
+    for (int i = 0; i < n; ++i) res += np_elem<T>(a, off + i, sq, mean);
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = np_elem<T>(a, off + j, sq, mean);
+  int i = 8;
+  for (; i < n - (n % 8); i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) r[j] += np_elem<T>(a, off + i + j, sq, mean);
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += np_elem<T>(a, off + i, sq, mean);
+  return res;
+}
+
+template <class T>
+__global__ __launch_bounds__(256) void np_buf_sums(const T* __restrict__ a, long long n,
+                                                   const double* __restrict__ meanp, int sq,
+                                                   double* __restrict__ bsum) {
+  __shared__ double leaf[4][kNpBuf / 32];
+  __shared__ int soff[4][24], sn[4][24], sst[4][24];
+  __shared__ double sleft[4][24];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long b = (long long)blockIdx.x * 4 + wv;
+  const long long nb = (n + kNpBuf - 1) / kNpBuf;
+  if (b >= nb) return;                             // whole waves; no block barrier below
+  const double mean = sq ? *meanp : 0.0;
+  const long long off = b * kNpBuf;
+  const int len = (int)(n - off < kNpBuf ? n - off : kNpBuf);
+  for (int k = lane; k < kNpBuf / 32; k += 64) {
+    const int wlo = 32 * k;
+    if (wlo >= len) break;
+    const int pos = wlo + 31 < len - 1 ? wlo + 31 : len - 1;
+    int no = 0, nn = len;
+    while (nn > 128) {                             // the leaf holding pos
+      int h = nn / 2;
+      h -= h % 8;
+      if (pos < no + h) nn = h;
+      else { no += h; nn -= h; }
+    }
+    if (no >= wlo) leaf[wv][no >> 5] = np_leaf<T>(a, off + no, nn, sq, mean);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+  if (lane != 0) return;
+  // post-order walk of the pairwise tree of [0, len)
+  int top = 0;
+  soff[wv][0] = 0;
+  sn[wv][0] = len;
+  sst[wv][0] = 0;
+  double ret = 0.0;
+  for (;;) {
+    const int o = soff[wv][top], m = sn[wv][top];
+    int h = m / 2;
+    h -= h % 8;
+    if (m <= 128) {
+      ret = leaf[wv][o >> 5];
+    } else if (sst[wv][top] == 0) {
+      sst[wv][top] = 1;
+      ++top;
+      soff[wv][top] = o;
+      sn[wv][top] = h;
+      sst[wv][top] = 0;
+      continue;
+    } else if (sst[wv][top] == 1) {
+      sleft[wv][top] = ret;
+      sst[wv][top] = 2;
+      ++top;
+      soff[wv][top] = o + h;
+      sn[wv][top] = m - h;
+      sst[wv][top] = 0;
+      continue;
+    } else {
+      ret = sleft[wv][top] + ret;
+    }
+    if (top == 0) break;
+    --top;
+  }
+  bsum[b] = ret;
+}
+
+// r = 0; r += bsum[k] in order; out[0] = r / n (mean) or out[1] = sqrt(r / n).
+__global__ __launch_bounds__(256) void np_finish(const double* __restrict__ bsum, long long nb,
+                                                 long long n, int sq, double* __restrict__ out) {
+  __shared__ double t[256];
+  const int tid = threadIdx.x;
+  double r = 0.0;
+  for (long long b0 = 0; b0 < nb; b0 += 256) {
+    __syncthreads();
+    if (b0 + tid < nb) t[tid] = bsum[b0 + tid];
+    __syncthreads();
+    if (tid == 0) {
+      const int m = nb - b0 < 256 ? (int)(nb - b0) : 256;
+      for (int k = 0; k < m; ++k) r += t[k];
+    }
+  }
+  if (tid == 0) {
+    const double q = r / (double)n;
+    if (sq) out[1] = sqrt(q);
+    else out[0] = q;
+  }
+}
+
+size_t np_stats_scratch_bytes(long long n) {
+  return (size_t)((n + kNpBuf - 1) / kNpBuf) * sizeof(double) + 64;
+}
+
+hipError_t launch_np_stats(int dtype, const void* a, long long n, double* out, void* scratch,
+                           hipStream_t st) {
+  if (n < 1 || !out || !scratch) return hipErrorInvalidValue;
+  const long long nb = (n + kNpBuf - 1) / kNpBuf;
+  const unsigned grid = (unsigned)((nb + 3) / 4);
+  double* bsum = static_cast<double*>(scratch);
+  for (int sq = 0; sq < 2; ++sq) {
+    switch (dtype) {
+      case VSIG_C128:
+        hipLaunchKernelGGL(np_buf_sums<double2>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const double2*>(a), n, out, sq, bsum);
+        break;
+      case VSIG_F64:
+        hipLaunchKernelGGL(np_buf_sums<double>, dim3(grid), dim3(256), 0, st,
+                           static_cast<const double*>(a), n, out, sq, bsum);
+        break;
+      default:
+        return hipErrorInvalidValue;
+    }
+    hipLaunchKernelGGL(np_finish, dim3(1), dim3(256), 0, st, bsum, nb, n, sq, out);
+  }
+  return hipGetLastError();
+}
+
 }  // namespace vsig

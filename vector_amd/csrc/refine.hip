@@ -6,20 +6,23 @@
 // over np.correlate's complex128 direct sums, cross_correlate_signals
 // utils.py:1279-1285) separates near-ties at the 1e-13 level: the reference's
 // own tone data (data/packet_*.mat against data/fixed_test_vector.mat) have
-// top-2 gaps of 1e-13 .. 7e-12 in |c|^2, 1e5 x below the fp32 error.  This
-// pass re-ranks, in double precision and in the caller's operand precision
-// (complex64 or complex128), every output whose fp32 |c| lies within a band
-// eps of the fp32 maximum:
+// top-2 gaps of 1e-13 .. 7e-12 in |c|^2, 1e5 x below the fp32 error, and a
+// tone against itself ties in exact arithmetic at every full-overlap lag.
+// This pass re-ranks every output whose fp32 |c| lies within a band eps of the
+// fp32 maximum, in numpy's own operation order and the caller's operand
+// precision (complex64 or complex128):
 //   select  : candidate items -- for the fused correlator, fused with the
 //             finalize of its wave partials into one launch (the last block
 //             to finish reduces, then selects): the thread columns whose lane
-//             key is in the band (64 outputs m(t) + TF q of one thread, where
+//             key is in the band (the outputs m(t) + TF q of one thread, where
 //             the kernel writes lane keys), else the waves whose partial max
 //             is (a wave covers ob + wstep w + l + 64 (q % rsub) + stride
 //             (q / rsub), see xcorr.hip); for a stored c64 array, its
-//             64-output chunks holding one;
-//   numpy   : every output of every item evaluated in numpy's own operation
-//             order -- np.correlate's complex128 dot is OpenBLAS zdotu (8 fma
+//             64-output chunks holding one.  Every item is kept (the scratch
+//             holds all of them) together with the span [lo, hi] of final
+//             outputs the items cover;
+//   numpy   : every candidate output evaluated in numpy's own operation order
+//             -- np.correlate's complex128 dot is OpenBLAS zdotu (8 fma
 //             accumulators per component over complex k mod 8, a fixed add
 //             tree, a scalar fma tail, re = d0 - d1, im = d2 + d3; above 10000
 //             terms split over T = blas_threads chunks added in order), |c| by
@@ -27,16 +30,31 @@
 //             larger) -- so every value is numpy's to the bit (oracle/npdot.c
 //             restates it on the CPU, tests/test_npdot_cpu.py pins it against
 //             numpy).  np.argmax's rule then applies as is: the max |c| and the
-//             lowest output index attaining it, by the last block, which
-//             replaces the peak record's max / index (sums untouched).  The
-//             operand windows go through LDS (the whole block loads a tile,
-//             the 8 lanes of zdot's slots consume it), so the sequential fma
-//             chains do not wait on a memory round trip per step;
-//   patch   : optionally the refined values into a complex128 c.
-// All sizes on the device (no host synchronisation); more than `cap` items
-// leaves the record as the fp32 pass produced it and sets status = 1.
-// Cross-block hand-offs (last block to finish) use one agent-scope fence per
-// block and agent-scope atomic loads of what other blocks wrote.
+//             lowest output index attaining it replace the peak record's max /
+//             index (sums untouched).  Two forms, chosen on the device:
+//               sparse (<= kSparseMax candidate outputs, or a span much wider
+//                 than the candidates): one output per block iteration, its
+//                 operand windows staged through LDS by the whole block, the 32
+//                 fma chains of zdot's slots on 32 lanes (latency form: the
+//                 usual handful of outputs around a planted peak);
+//               dense (flat |c|: a tone, a periodic vector of tone packets --
+//                 up to every output): every output of the span, 64
+//                 consecutive full-overlap outputs per wave; lane (c, s) runs
+//                 zdot slot s of the 8 outputs c + 8 r, 32 independent fma
+//                 chains, with the sliding operand held as an 8-element
+//                 register window (one new element per step serves all 8
+//                 outputs) -- throughput form, fp64-FMA bound.  The few
+//                 partial-overlap outputs of the span take the sparse form.
+//             No cap: the pass always finishes with numpy's answer; the
+//             "refine_cap" option is an explicit opt-in limit (status 1);
+//   patch   : optionally numpy's complex128 value of every evaluated output
+//             into a complex128 c.
+// The same dense kernel evaluates numpy's |c| of every output of a range into
+// an array (launch_refine_values: the exact confidence statistics of
+// find_correlation_peak on a flat |c|, see reduce.hip np_stats).
+// All sizes on the device (no host synchronisation).  Cross-block hand-offs
+// (last block to finish) use one agent-scope fence per block and agent-scope
+// atomic loads of what other blocks wrote.
 #include "os_common.hpp"
 
 namespace vsig {
@@ -51,6 +69,8 @@ template <> __device__ __forceinline__ double2 ld2<float2>(const float2* p, long
 template <> __device__ __forceinline__ double2 ld2<double2>(const double2* p, long long i) {
   return p[i];
 }
+__device__ __forceinline__ double2 to_d2(float2 v) { return make_double2((double)v.x, (double)v.y); }
+__device__ __forceinline__ double2 to_d2(double2 v) { return v; }
 
 // Overlap of output i (index into the 'full' correlation) with a: taps
 // k in [k0, k1), a index i - (nv - 1) + k.
@@ -65,13 +85,106 @@ __device__ __forceinline__ void tap_range(long long i, long long na, long long n
 // Shared scratch header (zeroed before select: by the fused finalize, or a memset).
 struct RefineKeys {
   unsigned long long count;    // candidate items appended by select
-  unsigned long long unused1;
-  unsigned long long max2;     // bits of numpy's max |c| (>= 0: integer order)
-  unsigned long long unused3;
-  unsigned long long status;   // 1: more than cap items (record left unrefined)
-  unsigned long long done;     // numpy-pass blocks finished (the last one finishes)
+  unsigned long long lo_inv;   // ~(lowest final output an item covers)  (atomic max)
+  unsigned long long hi_p1;    // highest final output an item covers + 1 (atomic max)
+  unsigned long long status;   // 1: more candidate outputs than the opt-in cap
+  unsigned long long done;     // numpy-pass blocks finished (the last one reduces)
+  unsigned long long pad[3];
 };
-static_assert(sizeof(RefineKeys) <= 64, "the items follow the keys at +64 B");
+static_assert(sizeof(RefineKeys) == 64, "the items follow the keys at +64 B");
+
+struct RefineSlot { double m; long long i; };   // one per numpy-pass block
+
+constexpr int kNpThreads = 256;
+constexpr int kNpGrid = 512;                   // 2 blocks per CU (64 KB of LDS each)
+constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
+constexpr long long kBlasThreadMin = 10000;    // zdotu_k: threads only above this n
+constexpr long long kSparseMax = 4096;         // candidate outputs of the sparse form
+
+struct RefineGeom {
+  long long nout;       // outputs (final space)
+  long long F;          // final output o is full-correlation index F + o
+  long long na, nv;     // np.correlate(a, v) operand lengths
+  int rev;              // raw (kernel) index -> final: nout - 1 - raw
+  int from_array;       // items are 64-output chunks of a stored array
+  long long hop;        // partial items: outputs per block, waves per block,
+  int waves, Q, stride; //   rows per item and their stride,
+  int wstep, rsub;      //   wave base step, 64-output rows per stride step
+  int cols;             // > 0: items are thread columns (wave p, column l) =
+                        //   p * 64 + l, cols rows each (xcorr_lane_keys)
+  int nthr;             // OpenBLAS threads of the numpy being matched (zdotu
+                        //   splits sums over 10000 terms into nthr chunks)
+  long long per_item;   // candidate outputs per item
+  long long cap;        // opt-in limit on candidate outputs (0: none)
+};
+
+__device__ __forceinline__ long long row_offset(const RefineGeom& g, int w, int q, int l) {
+  return (long long)g.wstep * w + l + 64LL * (q % g.rsub) + (long long)g.stride * (q / g.rsub);
+}
+
+// Final output of row q, lane l of wave partial p (-1: past the block's outputs).
+__device__ __forceinline__ long long item_output(const RefineGeom& g, long long p, int q, int l) {
+  const long long b = p / g.waves;
+  const int w = (int)(p - b * g.waves);
+  const long long ob = b * g.hop;
+  const long long rem = g.nout - ob;
+  const long long lim = rem < g.hop ? rem : g.hop;
+  const long long r = row_offset(g, w, q, l);
+  if (r >= lim) return -1;
+  const long long raw = ob + r;
+  return g.rev ? g.nout - 1 - raw : raw;
+}
+
+// Candidate output e (item e / per_item, its output e % per_item), -1: none.
+__device__ __forceinline__ long long entry_output(const RefineGeom& g, const long long* items,
+                                                  long long e) {
+  const long long it = e / g.per_item;
+  const int sub = (int)(e - it * g.per_item);
+  const long long item = items[it];
+  if (g.from_array) {
+    const long long raw = item * 64 + sub;
+    return raw < g.nout ? raw : -1;
+  }
+  if (g.cols) return item_output(g, item >> 6, sub, (int)(item & 63));
+  return item_output(g, item, sub >> 6, sub & 63);
+}
+
+// Final outputs [lo, hi] an item covers (rows are increasing in q and the
+// valid ones a prefix); false: none.
+__device__ __forceinline__ bool item_span(const RefineGeom& g, long long item, long long& lo,
+                                          long long& hi) {
+  long long rlo, rhi;
+  if (g.from_array) {
+    rlo = item * 64;
+    if (rlo >= g.nout) return false;
+    rhi = rlo + 63 < g.nout - 1 ? rlo + 63 : g.nout - 1;
+    lo = rlo;
+    hi = rhi;
+    return true;
+  }
+  const long long p = g.cols ? item >> 6 : item;
+  const int l = g.cols ? (int)(item & 63) : 0;
+  const long long b = p / g.waves;
+  const int w = (int)(p - b * g.waves);
+  const long long ob = b * g.hop;
+  const long long rem = g.nout - ob;
+  const long long lim = rem < g.hop ? rem : g.hop;
+  if (row_offset(g, w, 0, l) >= lim) return false;
+  int qh = (g.cols ? g.cols : g.Q) - 1;
+  while (row_offset(g, w, qh, l) >= lim) --qh;
+  rlo = ob + row_offset(g, w, 0, l);
+  long long top = row_offset(g, w, qh, l) + (g.cols ? 0 : 63);
+  if (top >= lim) top = lim - 1;
+  rhi = ob + top;
+  if (g.rev) {
+    lo = g.nout - 1 - rhi;
+    hi = g.nout - 1 - rlo;
+  } else {
+    lo = rlo;
+    hi = rhi;
+  }
+  return true;
+}
 
 __device__ __forceinline__ double band_threshold(const PeakPartial* rec, double eps) {
   const double t = rec->max2 * (1.0 - eps);     // finalized record: max |c|
@@ -80,16 +193,19 @@ __device__ __forceinline__ double band_threshold(const PeakPartial* rec, double 
 
 __global__ __launch_bounds__(256) void refine_select_array(
     const float2* __restrict__ c, long long nout, const PeakPartial* __restrict__ rec, double eps,
-    long long cap, long long* __restrict__ items, RefineKeys* __restrict__ keys) {
+    long long* __restrict__ items, RefineKeys* __restrict__ keys) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   const double t = band_threshold(rec, eps);
   const bool hit = i < nout && (double)hypotf(c[i].x, c[i].y) >= t;
   // one candidate per 64-output chunk: the chunk's lowest hitting lane appends
   const unsigned long long m = __ballot(hit);
   if (hit && (threadIdx.x & 63) == (unsigned)__builtin_ctzll(m)) {
+    const long long ch = i >> 6;
     const unsigned long long j = atomicAdd(&keys->count, 1ull);
-    if ((long long)j < cap) items[j] = i >> 6;
-    else atomicOr(&keys->status, 1ull);
+    items[j] = ch;
+    const long long hi = ch * 64 + 63 < nout - 1 ? ch * 64 + 63 : nout - 1;
+    atomicMax(&keys->lo_inv, ~(unsigned long long)(ch * 64));
+    atomicMax(&keys->hi_p1, (unsigned long long)(hi + 1));
   }
 }
 
@@ -105,9 +221,10 @@ struct FinalizeSelect {
   PeakPartial* tmp;                 // gridDim.x first-level records
   unsigned long long* done;         // zero between launches (reset here)
   PeakPartial* rec;                 // finalized record (max |c|)
-  double eps; long long cap;
+  double eps;
   long long* items; RefineKeys* keys;
   const unsigned* lkeys;            // optional lane keys (64 per wave partial)
+  RefineGeom g;                     // item -> output spans
 };
 
 // A record another block of this launch wrote (possibly on another XCD).
@@ -125,7 +242,7 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
   __shared__ int slast, ncl;
   __shared__ int clist[kFinalizeTmp];
   __shared__ double cmax[kFinalizeTmp];
-  __shared__ unsigned long long scount;
+  __shared__ unsigned long long scount, slo, shi;
   __shared__ double sthr;
   {
     const long long lo = (long long)blockIdx.x * f.chunk;
@@ -141,9 +258,6 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     }
     block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
   }
-#if VSIG_REFINE_KO == 5                            // tuning: the first level alone
-  return;
-#endif
   if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
     __threadfence();
     slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
@@ -174,14 +288,12 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
       *f.done = 0;
       ncl = 0;
       scount = 0;
+      slo = ~0ull;
+      shi = 0;
     }
     __syncthreads();
   }
   const double t2 = sthr;
-#if VSIG_REFINE_KO == 4                            // tuning: no candidate select
-  if (tid == 0) *f.keys = RefineKeys{};
-  return;
-#endif
   for (int k = tid; k < g1; k += 256)
     if (cmax[k] >= t2) clist[atomicAdd(&ncl, 1)] = k;
   __syncthreads();
@@ -189,6 +301,7 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
   // lane keys with one coalesced load and appends the in-band columns
   const int lane = tid & 63;
   const int nc = ncl;
+  unsigned long long mylo = ~0ull, myhi = 0;
   for (int c = 0; c < nc; ++c) {
     const long long lo = (long long)clist[c] * f.chunk;
     const long long hi = lo + f.chunk < f.nparts ? lo + f.chunk : f.nparts;
@@ -202,82 +315,50 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
       }
 #pragma unroll 1
       for (int q = 0; q < kPre; ++q) {
-      const long long pb = pb0 + 256LL * q;
-      unsigned long long hits = __ballot(pm[q] >= t2);
-      // past the cap the refine is skipped anyway (status 1): stop appending
-      // (a flat |c| puts every partial in the band)
-      if (*(volatile unsigned long long*)&scount > (unsigned long long)f.cap) hits = 0;
-      while (hits) {
-        const int src = __builtin_ctzll(hits);
-        hits &= hits - 1;
-        const long long hp = pb + src;
-        bool take;
-        long long item;
-        if (f.lkeys) {
-          take = (double)__uint_as_float(f.lkeys[hp * 64 + lane] & ~63u) >= t2;
-          item = hp * 64 + lane;
-        } else {
-          take = lane == src;
-          item = hp;
+        const long long pb = pb0 + 256LL * q;
+        unsigned long long hits = __ballot(pm[q] >= t2);
+        while (hits) {
+          const int src = __builtin_ctzll(hits);
+          hits &= hits - 1;
+          const long long hp = pb + src;
+          bool take;
+          long long item;
+          if (f.lkeys) {
+            take = (double)__uint_as_float(f.lkeys[hp * 64 + lane] & ~63u) >= t2;
+            item = hp * 64 + lane;
+          } else {
+            take = lane == src;
+            item = hp;
+          }
+          const unsigned long long km = __ballot(take);
+          unsigned long long j0 = 0;
+          if (lane == 0) j0 = atomicAdd(&scount, (unsigned long long)__popcll(km));
+          j0 = __shfl(j0, 0);
+          const unsigned long long j = j0 + __popcll(km & ((1ull << lane) - 1));
+          if (take) {
+            f.items[j] = item;
+            long long ilo, ihi;
+            if (item_span(f.g, item, ilo, ihi)) {
+              mylo = (unsigned long long)ilo < mylo ? (unsigned long long)ilo : mylo;
+              myhi = (unsigned long long)ihi + 1 > myhi ? (unsigned long long)ihi + 1 : myhi;
+            }
+          }
         }
-        const unsigned long long km = __ballot(take);
-        unsigned long long j0 = 0;
-        if (lane == 0) j0 = atomicAdd(&scount, (unsigned long long)__popcll(km));
-        j0 = __shfl(j0, 0);
-        const unsigned long long j = j0 + __popcll(km & ((1ull << lane) - 1));
-        if (take && (long long)j < f.cap) f.items[j] = item;
-      }
       }
     }
-    __syncthreads();
-    if (scount > (unsigned long long)f.cap) break;   // uniform
+  }
+  if (myhi) {
+    atomicMin(&slo, mylo);
+    atomicMax(&shi, myhi);
   }
   __syncthreads();
   if (tid == 0) {
     RefineKeys z{};
     z.count = scount;
-    z.status = (long long)scount > f.cap ? 1ull : 0ull;
+    z.lo_inv = ~slo;
+    z.hi_p1 = shi;
     *f.keys = z;
   }
-}
-
-struct RefineGeom {
-  long long nout;       // outputs (final space)
-  long long F;          // final output o is full-correlation index F + o
-  long long na, nv;     // np.correlate(a, v) operand lengths
-  int rev;              // raw (kernel) index -> final: nout - 1 - raw
-  int from_array;       // items are 64-output chunks of a stored array
-  long long hop;        // partial items: outputs per block, waves per block,
-  int waves, Q, stride; //   rows per item and their stride,
-  int wstep, rsub;      //   wave base step, 64-output rows per stride step
-  int cols;             // > 0: items are thread columns (wave p, column l) =
-                        //   p * 64 + l, cols rows each (xcorr_lane_keys)
-  int nthr;             // OpenBLAS threads of the numpy being matched (zdotu
-                        //   splits sums over 10000 terms into nthr chunks)
-};
-
-__device__ __forceinline__ long long item_output(const RefineGeom& g, long long item, int q, int l) {
-  long long raw;
-  if (g.from_array) {
-    raw = item * 64 + l;
-    return raw < g.nout ? raw : -1;
-  }
-  const long long b = item / g.waves;
-  const int w = (int)(item - b * g.waves);
-  const long long ob = b * g.hop;
-  const long long rem = g.nout - ob;
-  const long long lim = rem < g.hop ? rem : g.hop;
-  const long long r = (long long)g.wstep * w + l + 64LL * (q % g.rsub) + (long long)g.stride * (q / g.rsub);
-  if (r >= lim) return -1;
-  raw = ob + r;
-  return g.rev ? g.nout - 1 - raw : raw;
-}
-
-// Output po (< 64) of unit qu of an item: a wave item's unit qu is its row q
-// (64 outputs l); a column item has one unit, its rows q = po.
-__device__ __forceinline__ long long unit_output(const RefineGeom& g, long long item, int qu, int po) {
-  if (g.cols) return po < g.cols ? item_output(g, item >> 6, po, (int)(item & 63)) : -1;
-  return item_output(g, item, qu, po);
 }
 
 // One zdot_compute over chunk [c0, c0 + w) of output i's overlap (x = a +
@@ -289,13 +370,6 @@ __device__ __forceinline__ long long unit_output(const RefineGeom& g, long long 
 // reads.  The add tree combines the slots as the kernel does ((s, s^2), then
 // (s, s^4), then the two 128-bit halves: s, s^1); lane 0 gathers the four
 // sums and runs the scalar tail.  Result in lane 0.
-#ifndef VSIG_REFINE_KO
-#define VSIG_REFINE_KO 0
-#endif
-constexpr int kNpThreads = 256;
-constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
-constexpr long long kBlasThreadMin = 10000;   // zdotu_k: threads only above this n
-
 template <class T>
 __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* __restrict__ v,
                                               long long ax, long long c0, long long w,
@@ -323,9 +397,6 @@ __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* 
       ys[q] = in ? v[c0 + tb + j] : T{};
     }
   };
-#if VSIG_REFINE_KO == 2                            // tuning: no staging loads
-  if (n8 > 0) return;
-#endif
   if (n8 > 0) fetch(0);
   for (long long tb = 0; tb < n8; tb += kTile) {  // uniform
     const int tl = n8 - tb < kTile ? (int)(n8 - tb) : kTile;
@@ -340,12 +411,10 @@ __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* 
     }
     __syncthreads();
     if (tb + kTile < n8) fetch(tb + kTile);
-#if VSIG_REFINE_KO != 1                            // tuning: no fma chains
     if (tid < 32) {
 #pragma unroll 16
       for (int k = s; k < tl; k += 8) acc = fma(X[k], Y[k], acc);
     }
-#endif
   }
   if (tid < 32) {                                 // lanes 0..31 of wave 0
     acc = acc + __shfl_xor(acc, 2, 8);
@@ -372,180 +441,369 @@ __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* 
   }
 }
 
-// Every candidate output (entry e = u * 64 + po of unit u of an item), one
-// per block iteration: numpy's complex128 value and |c|, the max |c| by a
-// 64-bit atomic max; the last block to finish takes the lowest output index
-// attaining it (np.argmax's first-max rule) and writes the record.
+// OpenBLAS's split of an nt-term zdot over its threads (zdotu_k: only above
+// 10000 terms): chunk t of nch.
+__device__ __forceinline__ int blas_chunks(long long nt, int nthr) {
+  return (nt <= kBlasThreadMin || nthr <= 1) ? 1 : nthr;
+}
+
+// numpy's complex128 c[o] by the whole block (result in thread 0).
 template <class T>
-__global__ __launch_bounds__(kNpThreads) void refine_numpy(const T* __restrict__ a, const T* __restrict__ v,
-                                                         RefineGeom g, const long long* __restrict__ items,
-                                                         long long cap, RefineKeys* __restrict__ keys,
-                                                         double* __restrict__ vals,
-                                                         long long* __restrict__ oidx,
-                                                         double2* __restrict__ cv,
-                                                         PeakPartial* __restrict__ rec) {
-  const long long cnt = (long long)keys->count;
-  if (keys->status || cnt == 0) return;            // uniform: no block counts itself
-#if VSIG_REFINE_KO == 3 || VSIG_REFINE_KO == 5     // tuning: the launch alone
-  return;
-#endif
-  const long long n = (cnt < cap ? cnt : cap) * g.Q * 64;
-  // blocks past the entry count take no part (the last-block hand-off counts
-  // only the nact blocks that have entries)
-  const long long nact = n < (long long)gridDim.x ? n : (long long)gridDim.x;
-  if ((long long)blockIdx.x >= nact) return;
+__device__ __forceinline__ void eval_single(const T* __restrict__ a, const T* __restrict__ v,
+                                            const RefineGeom& g, long long o, double* tiles,
+                                            double& re, double& im) {
+  const long long i = g.F + o;
+  long long k0, k1;
+  tap_range(i, g.na, g.nv, k0, k1);
+  const long long nt = k1 - k0;
+  const long long ax = i - (g.nv - 1);
+  const int nch = blas_chunks(nt, g.nthr);
+  re = 0.0;
+  im = 0.0;
+  long long rest = nt, c0 = k0;
+  for (int t = 0; t < nch && rest > 0; ++t) {    // OpenBLAS threads' chunks, in order
+    long long wd = (rest + (nch - t) - 1) / (nch - t);
+    if (wd > rest) wd = rest;
+    double pr = 0.0, pi = 0.0;
+    np_zdot_chunk<T>(a, v, ax, c0, wd, tiles, pr, pi);
+    re = re + pr;
+    im = im + pi;
+    c0 += wd;
+    rest -= wd;
+  }
+  re = 0.0 + re;                                   // numpy's CDOUBLE_dot sum
+  im = 0.0 + im;
+}
+
+// numpy's complex128 c[o] for the 64 consecutive full-overlap outputs
+// ob + c + 8 r (lane = 8 c + s, r < 8) of one wave; lane (c, s) returns output
+// ob + c + 8 s.  Term t of output o is x = a[xa(o) + t], y = conj(v[yv(o) + t]),
+// t < wf = min(na, nv); D = +1 (na >= nv): xa = o + F - (nv - 1), yv = 0 (a
+// slides); D = -1: xa = 0, yv = (nv - 1) - (o + F) (v slides, backwards).
+// Slot s of zdot's 8-way split covers t = c0 + s + 8 j of each chunk; for the
+// lane's outputs r the sliding operand at step j is element m = j + D r of
+// the lane's sequence S[B + 8 m], so the 8 outputs share one register window
+// of 8 elements that advances by one element per step (loaded a block of 8
+// steps ahead); the fixed operand's element c0 + s + 8 j is shared by all
+// outputs of the block and staged through LDS (tiles of 4096 elements, the
+// block's 4 waves step through the same tiles).
+template <class T, int D>
+__device__ __forceinline__ void eval_group(const T* __restrict__ a, const T* __restrict__ v,
+                                           const RefineGeom& g, long long ob, long long wf,
+                                           double* tiles, double& re_out, double& im_out) {
+  const int lane = threadIdx.x & 63, c = lane >> 3, s = lane & 7;
+  const T* S = D > 0 ? a : v;
+  const T* X = D > 0 ? v : a;
+  const long long ns = D > 0 ? g.na : g.nv;
+  const long long sb = D > 0 ? ob + g.F - (g.nv - 1) : (g.nv - 1) - (ob + g.F);
+  double2* xs = reinterpret_cast<double2*>(tiles);
+  constexpr long long kXT = 2 * kTile;             // fixed-operand elements per LDS tile
+  const int nch = blas_chunks(wf, g.nthr);
+  double re = 0.0, im = 0.0;
+  long long rest = wf, c0 = 0;
+  for (int t = 0; t < nch && rest > 0; ++t) {    // uniform
+    long long wd = (rest + (nch - t) - 1) / (nch - t);
+    if (wd > rest) wd = rest;
+    const long long n8 = wd & ~7LL;
+    const long long B = (D > 0 ? sb + c : sb - c) + s + c0;
+    // indices clamped into the operand (lanes of outputs past the range and
+    // loads past the last step read a valid element they do not use)
+    auto sl = [&](long long m) {
+      long long i = B + 8 * m;
+      i = i < 0 ? 0 : i;
+      return S[i < ns ? i : ns - 1];
+    };
+    double acc[8][4];
+#pragma unroll
+    for (int r = 0; r < 8; ++r)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc[r][k] = 0.0;
+    double2 ring[8];
+    T P[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int m = D > 0 ? k : k - 7;             // window at step 0
+      ring[m & 7] = to_d2(sl(m));
+      P[k] = sl(D > 0 ? k + 8 : k + 1);            // inserted after step k
+    }
+    for (long long tb = 0; tb < n8; tb += kXT) {   // uniform across the block
+      const long long tl = n8 - tb < kXT ? n8 - tb : kXT;
+      __syncthreads();                             // the previous tile is consumed
+      for (int i = threadIdx.x; i < tl; i += kNpThreads) xs[i] = to_d2(X[c0 + tb + i]);
+      __syncthreads();
+      const long long j0 = tb >> 3, j1 = (tb + tl) >> 3;   // this tile's steps
+      for (long long J0 = j0; J0 < j1; J0 += 8) {   // uniform
+        T Pn[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) Pn[k] = sl(D > 0 ? J0 + 16 + k : J0 + 9 + k);
+#pragma unroll
+        for (int jj = 0; jj < 8; ++jj) {
+          if (J0 + jj < j1) {                        // uniform
+            const double2 f = xs[(J0 + jj - j0) * 8 + s];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+              const double2 e = ring[(D > 0 ? jj + r : jj - r) & 7];
+              const double2 x = D > 0 ? e : f;
+              const double2 y = D > 0 ? f : e;
+              const double yn = -y.y;
+              acc[r][0] = fma(x.x, y.x, acc[r][0]);
+              acc[r][1] = fma(x.y, yn, acc[r][1]);
+              acc[r][2] = fma(x.x, yn, acc[r][2]);
+              acc[r][3] = fma(x.y, y.x, acc[r][3]);
+            }
+          }
+          ring[(D > 0 ? jj : jj + 1) & 7] = to_d2(P[jj]);
+        }
+#pragma unroll
+        for (int k = 0; k < 8; ++k) P[k] = Pn[k];
+      }
+    }
+    // zdot's add tree over the 8 slots (lanes 8 c + s, s < 8), then lane s
+    // keeps output r = s
+    double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      double q[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        double u = acc[r][k];
+        u = u + __shfl_xor(u, 2, 8);
+        u = u + __shfl_xor(u, 4, 8);
+        u = u + __shfl_xor(u, 1, 8);
+        q[k] = u;
+      }
+      if (r == s) { d0 = q[0]; d1 = q[1]; d2 = q[2]; d3 = q[3]; }
+    }
+    const long long o = ob + c + 8 * s;
+    const long long xo = D > 0 ? o + g.F - (g.nv - 1) : 0;
+    const long long yo = D > 0 ? 0 : (g.nv - 1) - (o + g.F);
+    for (long long tt = n8; tt < wd; ++tt) {        // scalar tail (uniform trip count)
+      long long ia = xo + c0 + tt, iv = yo + c0 + tt;
+      ia = ia < 0 ? 0 : (ia < g.na ? ia : g.na - 1);
+      iv = iv < 0 ? 0 : (iv < g.nv ? iv : g.nv - 1);
+      const double2 x = ld2<T>(a, ia), y = ld2<T>(v, iv);
+      const double yi = -y.y;
+      d0 = fma(x.x, y.x, d0);
+      d1 = fma(x.y, yi, d1);
+      d2 = fma(x.x, yi, d2);
+      d3 = fma(y.x, x.y, d3);
+    }
+    double rr = d0 - d1;
+    const double mm = d2 + d3;
+    rr = fma(mm, 0.0, rr);
+    re = re + rr;
+    im = im + mm;
+    c0 += wd;
+    rest -= wd;
+  }
+  re_out = 0.0 + re;
+  im_out = 0.0 + im;
+}
+
+// The numpy pass.  Candidate mode (vals == nullptr): the select's items;
+// values mode: every output of [vlo, vhi], |c| into vals[o - vlo].  Every
+// evaluated output updates the block's (max |c|, lowest index); the last block
+// to finish writes numpy's argmax into rec.
+template <class T>
+__global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
+    const T* __restrict__ a, const T* __restrict__ v, RefineGeom g, const long long* __restrict__ items,
+    RefineKeys* __restrict__ keys, RefineSlot* __restrict__ slots, double2* __restrict__ cv,
+    double* __restrict__ vals, long long vlo, long long vhi, PeakPartial* __restrict__ rec) {
   const int tid = threadIdx.x;
+  long long lo, hi, n;
+  bool dense;
+  if (vals) {
+    lo = vlo;
+    hi = vhi;
+    n = hi - lo + 1;
+    dense = true;
+  } else {
+    const long long cnt = (long long)keys->count;
+    if (cnt == 0) return;                          // uniform: no block counts itself
+    n = cnt * g.per_item;
+    if (g.cap > 0 && n > g.cap) {                  // opt-in limit: record left fp32
+      if (blockIdx.x == 0 && tid == 0) keys->status = 1;
+      return;
+    }
+    lo = (long long)~keys->lo_inv;
+    hi = (long long)keys->hi_p1 - 1;
+    dense = n > kSparseMax && hi - lo + 1 <= 8 * n;
+  }
+  // full-overlap (interior) outputs of the span
+  const long long wf = g.na < g.nv ? g.na : g.nv;
+  const long long i1 = (g.na < g.nv ? g.nv : g.na) - 1;
+  long long ilo = wf - 1 - g.F, ihi = i1 - g.F;
+  ilo = ilo > lo ? ilo : lo;
+  ihi = ihi < hi ? ihi : hi;
+  const long long nin = (dense && ihi >= ilo) ? ihi - ilo + 1 : 0;
+  const long long ngroups = (nin + 255) / 256;
+  const long long nleft = dense ? (nin ? ilo - lo : hi - lo + 1) : 0;
+  const long long nright = (dense && nin) ? hi - ihi : 0;
+  const long long ntask = dense ? ngroups + nleft + nright : n;
+  // blocks past the task count take no part (the last-block hand-off counts
+  // only the nact blocks that have work)
+  const long long nact = ntask < (long long)gridDim.x ? ntask : (long long)gridDim.x;
+  if ((long long)blockIdx.x >= nact) return;
   __shared__ double tiles[4 * kTile];
   __shared__ int slast;
-  __shared__ long long smin;
-  for (long long e = blockIdx.x; e < n; e += gridDim.x) {   // uniform per block
-    const long long u = e >> 6;
-    const int po = (int)(e & 63);
-    const long long o = unit_output(g, items[u / g.Q], (int)(u % g.Q), po);
-    if (o < 0) {
-      if (tid == 0) { vals[e] = -1.0; oidx[e] = -1; }
-      continue;
-    }
-    const long long i = g.F + o;
-    long long k0, k1;
-    tap_range(i, g.na, g.nv, k0, k1);
-    const long long nt = k1 - k0;
-    const long long ax = i - (g.nv - 1);
-    const int nch = (nt <= kBlasThreadMin || g.nthr <= 1) ? 1 : g.nthr;
-    double re = 0.0, im = 0.0;
-    long long rest = nt, c0 = k0;
-    for (int t = 0; t < nch && rest > 0; ++t) {    // OpenBLAS threads' chunks, in order
-      long long wd = (rest + (nch - t) - 1) / (nch - t);
-      if (wd > rest) wd = rest;
-      double pr = 0.0, pi = 0.0;
-      np_zdot_chunk<T>(a, v, ax, c0, wd, tiles, pr, pi);
-      re = re + pr;
-      im = im + pi;
-      c0 += wd;
-      rest -= wd;
-    }
-    if (tid == 0) {
-      re = 0.0 + re;                               // numpy's CDOUBLE_dot sum
-      im = 0.0 + im;
-      const double av = np_cabs(re, im);
-      vals[e] = av;
-      oidx[e] = o;
-      cv[e] = make_double2(re, im);
-      atomicMax(&keys->max2, (unsigned long long)__double_as_longlong(av));
+  __shared__ double wm[kNpThreads / 64];
+  __shared__ long long wi[kNpThreads / 64];
+  double bm = -1.0;
+  long long bi = 0x7fffffffffffffffLL;
+  auto record = [&](long long o, double re, double im) {
+    const double av = np_cabs(re, im);
+    betterd(bm, bi, av, o);
+    if (cv) cv[o] = make_double2(re, im);
+    if (vals) vals[o - lo] = av;
+  };
+  for (long long t = blockIdx.x; t < ntask; t += gridDim.x) {   // uniform per block
+    if (dense && t < ngroups) {
+      const long long ob = ilo + 256 * t + 64 * (tid >> 6);
+      double re, im;
+      if (g.na >= g.nv) eval_group<T, 1>(a, v, g, ob, wf, tiles, re, im);
+      else eval_group<T, -1>(a, v, g, ob, wf, tiles, re, im);
+      const long long o = ob + ((tid & 63) >> 3) + 8 * (tid & 7);
+      if (o <= ihi) record(o, re, im);
+    } else {
+      long long o;
+      if (dense) {
+        const long long e = t - ngroups;
+        o = e < nleft ? lo + e : ihi + 1 + (e - nleft);
+      } else {
+        o = entry_output(g, items, t);
+        if (o < 0) continue;
+      }
+      double re, im;
+      eval_single<T>(a, v, g, o, tiles, re, im);
+      if (tid == 0) record(o, re, im);
     }
   }
-  // the last block to finish: argmin over the entries, then the record (one
-  // release per block: thread 0 made every store of this block)
+  // the block's (max, lowest index), then the last block to finish reduces
+  // the nact block slots (one release per block)
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const double om = __shfl_xor(bm, off);
+    const long long oi = __shfl_xor(bi, off);
+    betterd(bm, bi, om, oi);
+  }
+  if ((tid & 63) == 0) {
+    wm[tid >> 6] = bm;
+    wi[tid >> 6] = bi;
+  }
   __syncthreads();
   if (tid == 0) {
+    for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
+    slots[blockIdx.x] = RefineSlot{bm, bi};
     __threadfence();
     slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
     if (slast) __threadfence();
-    smin = 0x7fffffffffffffffLL;
   }
   __syncthreads();
   if (!slast) return;
-  const double m2 = __longlong_as_double(
-      (long long)__hip_atomic_load(&keys->max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-  long long mi = 0x7fffffffffffffffLL;
-  for (long long q = tid; q < n; q += kNpThreads) {
-    const double ve = __hip_atomic_load(&vals[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (ve == m2 && ve >= 0.0) {
-      const long long o = __hip_atomic_load(&oidx[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      mi = o < mi ? o : mi;
-    }
+  bm = -1.0;
+  bi = 0x7fffffffffffffffLL;
+  for (long long q = tid; q < nact; q += kNpThreads) {
+    const double m = __hip_atomic_load(&slots[q].m, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const long long i = __hip_atomic_load(&slots[q].i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    betterd(bm, bi, m, i);
   }
+#pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
-    const long long om = __shfl_xor(mi, off);
-    mi = om < mi ? om : mi;
+    const double om = __shfl_xor(bm, off);
+    const long long oi = __shfl_xor(bi, off);
+    betterd(bm, bi, om, oi);
   }
-  if ((tid & 63) == 0) atomicMin(&smin, mi);
   __syncthreads();
-  if (tid == 0 && smin != 0x7fffffffffffffffLL) {
-    rec->max2 = m2;                                // numpy's |c| at its argmax
-    rec->idx = smin;
+  if ((tid & 63) == 0) {
+    wm[tid >> 6] = bm;
+    wi[tid >> 6] = bi;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
+    if (rec && bm >= 0.0) {
+      rec->max2 = bm;                              // numpy's |c| at its argmax
+      rec->idx = bi;
+    }
+    keys->done = 0;
   }
 }
 
-// Refined values into a complex128 output (stage-2 values where computed,
-// else the plain fp64 stage-1 sums; both beat the fp32 array they replace).
-__global__ __launch_bounds__(256) void refine_patch(long long cap, int Q,
-                                                    const RefineKeys* __restrict__ keys,
-                                                    const long long* __restrict__ oidx,
-                                                    const double2* __restrict__ cv,
-                                                    double2* __restrict__ out) {
-  const long long cnt = (long long)keys->count;
-  if (keys->status || cnt == 0) return;
-  const long long n = (cnt < cap ? cnt : cap) * Q * 64;
-  const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long e = (long long)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += stride) {
-    const long long o = oidx[e];
-    if (o >= 0) out[o] = cv[e];
-  }
+static RefineGeom make_geom(const RefineArgs& r) {
+  RefineGeom g{r.nout, r.F, r.na, r.nv, r.rev, r.from_array, r.hop, r.waves, r.Q, r.stride,
+               r.wstep, r.rsub, r.cols, r.blas_threads > 1 ? r.blas_threads : 1, 0, r.cap};
+  g.per_item = r.from_array ? 64 : r.cols ? r.cols : (long long)r.Q * 64;
+  return g;
 }
 
-size_t refine_scratch_bytes(long long cap_items, int Q) {
-  const long long n = cap_items * Q * 64;
-  return sizeof(RefineKeys) + 64 + (size_t)n * (8 + 8 + 16);
+static long long max_items(const RefineArgs& r) {
+  if (r.from_array) return (r.nout + 63) / 64;
+  return r.cols ? r.nparts * 64 : r.nparts;
+}
+
+size_t refine_scratch_bytes(const RefineArgs& r) {
+  return sizeof(RefineKeys) + (size_t)max_items(r) * 8 + kNpGrid * sizeof(RefineSlot);
+}
+
+static hipError_t launch_numpy(const RefineArgs& r, const RefineGeom& g, const long long* items,
+                               RefineKeys* keys, RefineSlot* slots, double* vals, long long vlo,
+                               long long vhi, hipStream_t st) {
+  auto go = [&](auto tag) {
+    using T = decltype(tag);
+    hipLaunchKernelGGL(refine_numpy<T>, dim3(kNpGrid), dim3(kNpThreads), 0, st,
+                       static_cast<const T*>(r.a), static_cast<const T*>(r.v), g, items, keys,
+                       slots, static_cast<double2*>(r.out128), vals, vlo, vhi, r.rec);
+  };
+  if (r.c128) go(double2{});
+  else go(float2{});
+  return hipGetLastError();
 }
 
 hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
-  if (r.cap_items < 1 || (r.cols && (r.from_array || r.cols > 64))) return hipErrorInvalidValue;
+  if (r.cols && (r.from_array || r.cols > 64)) return hipErrorInvalidValue;
   char* base = static_cast<char*>(r.scratch);
   RefineKeys* keys = reinterpret_cast<RefineKeys*>(base);
-  const long long n = r.cap_items * r.Q * 64;
-  long long* items = reinterpret_cast<long long*>(base + 64);
-  double* vals = reinterpret_cast<double*>(items + r.cap_items);
-  long long* oidx = reinterpret_cast<long long*>(vals + n);
-  double2* cv = reinterpret_cast<double2*>(oidx + n);
-  RefineGeom g{r.nout, r.F, r.na, r.nv, r.rev, r.from_array, r.hop, r.waves, r.Q, r.stride,
-               r.wstep, r.rsub, r.cols, r.blas_threads > 1 ? r.blas_threads : 1};
-  PeakPartial* rec = r.rec;
+  long long* items = reinterpret_cast<long long*>(base + sizeof(RefineKeys));
+  RefineSlot* slots = reinterpret_cast<RefineSlot*>(items + max_items(r));
+  const RefineGeom g = make_geom(r);
   if (r.finalize) {              // the partials' finalize + select in one launch
     if (r.from_array || !r.tmp || !r.done) return hipErrorInvalidValue;
-#ifndef VSIG_FIN_CHUNK
-#define VSIG_FIN_CHUNK 1024
-#endif
-    long long g1 = (r.nparts + VSIG_FIN_CHUNK - 1) / VSIG_FIN_CHUNK;
+    constexpr long long kFinChunk = 1024;   // wave partials per first-level block
+    long long g1 = (r.nparts + kFinChunk - 1) / kFinChunk;
     if (g1 < 1) g1 = 1;
     if (g1 > kFinalizeTmp) g1 = kFinalizeTmp;
     long long chunk = (r.nparts + g1 - 1) / g1;
     if (chunk < 1) chunk = 1;
     g1 = (r.nparts + chunk - 1) / chunk;
     if (g1 < 1) g1 = 1;
-    const FinalizeSelect f{r.parts, r.nparts, chunk, r.tmp, r.done, rec, r.eps, r.cap_items,
-                           items, keys, r.lkeys};
+    const FinalizeSelect f{r.parts, r.nparts, chunk, r.tmp, r.done, r.rec, r.eps, items, keys,
+                           r.lkeys, g};
     hipLaunchKernelGGL(refine_finalize_select, dim3((unsigned)g1), dim3(256), 0, st, f);
   } else {
-    if (r.cols || r.lkeys) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
-    if (e != hipSuccess) return e;
     // a stored c64 array (the correlator's partials are finalized and
     // selected by refine_finalize_select above)
-    if (!r.from_array) return hipErrorInvalidValue;
+    if (r.cols || r.lkeys || !r.from_array) return hipErrorInvalidValue;
+    hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
+    if (e != hipSuccess) return e;
     const long long grid = (r.nout + 255) / 256;
     hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
-                       rec, r.eps, r.cap_items, items, keys);
+                       r.rec, r.eps, items, keys);
   }
-  // one output per block iteration (grid-stride over the device-side count),
-  // capped so that the usual 64 candidate outputs get a block each
-#ifndef VSIG_REFINE_GRID
-#define VSIG_REFINE_GRID 256
-#endif
-  const long long gl = n < VSIG_REFINE_GRID ? n : VSIG_REFINE_GRID;
-  const unsigned gn = (unsigned)(gl > 0 ? gl : 1);
-  auto stages = [&](auto tag) {
-    using T = decltype(tag);
-    hipLaunchKernelGGL(refine_numpy<T>, dim3(gn), dim3(kNpThreads), 0, st, static_cast<const T*>(r.a),
-                       static_cast<const T*>(r.v), g, items, r.cap_items, keys, vals, oidx, cv, rec);
-  };
-  if (r.c128) stages(double2{});
-  else stages(float2{});
-  const unsigned g2 = gn;
-  if (r.out128)
-    hipLaunchKernelGGL(refine_patch, dim3(g2), dim3(256), 0, st, r.cap_items, r.Q, keys, oidx, cv,
-                       static_cast<double2*>(r.out128));
-  return hipGetLastError();
+  return launch_numpy(r, g, items, keys, slots, nullptr, 0, 0, st);
+}
+
+size_t refine_values_scratch_bytes() { return sizeof(RefineKeys) + kNpGrid * sizeof(RefineSlot); }
+
+hipError_t launch_refine_values(const RefineArgs& r, long long lo, long long hi, double* vals,
+                                hipStream_t st) {
+  if (!vals || lo < 0 || hi < lo || hi >= r.nout) return hipErrorInvalidValue;
+  RefineKeys* keys = static_cast<RefineKeys*>(r.scratch);
+  RefineSlot* slots = reinterpret_cast<RefineSlot*>(keys + 1);
+  hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
+  if (e != hipSuccess) return e;
+  RefineArgs q = r;
+  q.from_array = 1;                                // geometry unused in values mode
+  return launch_numpy(q, make_geom(q), nullptr, keys, slots, vals, lo, hi, st);
 }
 
 // ---------------------------------------------------------------------------

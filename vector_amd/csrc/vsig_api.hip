@@ -33,9 +33,13 @@ struct vsig_ctx {
   size_t rscratch_bytes = 0;
   void* lkeys = nullptr;                 // correlator lane keys (refine column candidates)
   size_t lkeys_bytes = 0;
+  void* vscratch = nullptr;              // numpy-order |c| of every output (exact stats)
+  size_t vscratch_bytes = 0;
+  void* sscratch = nullptr;              // np_stats buffer sums
+  size_t sscratch_bytes = 0;
   int refine = 1;                        // exact re-rank of the correlators' peak
   int refine_eps_ppm = 1000;             // fp32 candidate band (relative, ppm of max |c|)
-  long long refine_cap = 1LL << 20;      // max outputs revisited (else record left fp32)
+  long long refine_cap = 0;              // opt-in limit on candidate outputs (0: none)
   int blas_threads = 1;                  // numpy's OpenBLAS threads (its zdotu splits > 10000 terms)
   bool refine_ran = false;
   struct Chirp { long long M; float2* c; float2* B; };
@@ -310,9 +314,8 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
   }
   r.eps = c->refine_eps_ppm * 1e-6;
   r.blas_threads = c->blas_threads;
-  r.cap_items = c->refine_cap / (64LL * r.Q);
-  if (r.cap_items < 1) r.cap_items = 1;
-  int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, vsig::refine_scratch_bytes(r.cap_items, r.Q));
+  r.cap = c->refine_cap;
+  int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, vsig::refine_scratch_bytes(r));
   if (rc) return rc;
   r.scratch = c->rscratch;
   r.rec = rec;
@@ -522,6 +525,8 @@ void vsig_free(vsig_ctx* c) {
   for (int i = 0; i < 3; ++i) if (c->conv[i]) (void)hipFree(c->conv[i]);
   if (c->rscratch) (void)hipFree(c->rscratch);
   if (c->lkeys) (void)hipFree(c->lkeys);
+  if (c->vscratch) (void)hipFree(c->vscratch);
+  if (c->sscratch) (void)hipFree(c->sscratch);
   for (auto& kv : c->chirps) { (void)hipFree(kv.second.c); (void)hipFree(kv.second.B); }
   if (c->bigtmp) (void)hipFree(c->bigtmp);
   for (int i = 0; i < 2; ++i) if (c->spec[i]) (void)hipFree(c->spec[i]);
@@ -548,7 +553,7 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
     if (value < 1 || value > 500000) return fail(c, VSIG_E_INVALID, "refine_eps_ppm must be in [1, 500000]");
     c->refine_eps_ppm = value;
   } else if (k == "refine_cap") {
-    if (value < 4096) return fail(c, VSIG_E_INVALID, "refine_cap must be >= 4096");
+    if (value != 0 && value < 4096) return fail(c, VSIG_E_INVALID, "refine_cap must be 0 or >= 4096");
     c->refine_cap = value;
   } else if (k == "blas_threads") {
     if (value < 1 || value > 1024) return fail(c, VSIG_E_INVALID, "blas_threads must be in [1, 1024]");
@@ -581,10 +586,10 @@ int vsig_refine_status(vsig_ctx* c, int32_t* status, int64_t* candidates) {
   *status = 2;
   *candidates = 0;
   if (!c->refine_ran || !c->rscratch) return VSIG_OK;
-  unsigned long long keys[5];
+  unsigned long long keys[4];     // refine.hip RefineKeys: count, lo_inv, hi_p1, status
   HIPCHK(c, hipMemcpyAsync(keys, c->rscratch, sizeof(keys), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  *status = keys[4] ? 1 : 0;
+  *status = keys[3] ? 1 : 0;
   *candidates = (int64_t)keys[0];
   return VSIG_OK;
 }
@@ -1263,6 +1268,52 @@ int vsig_peak(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, vsig_peak_t*
   if (rc) return rc;
   HIPCHK(c, hipMemcpyAsync(peak, c->result, sizeof(vsig_peak_t), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+// numpy's np.mean / np.std of |a| (find_correlation_peak's mean_corr /
+// std_corr, utils.py:1329-1330) in numpy's own summation order.
+int vsig_abs_stats_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t n, double* stats_dev) {
+  if (!c || !a || !stats_dev) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (n < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  if (dtype != VSIG_DTYPE_C128 && dtype != VSIG_DTYPE_F64)
+    return fail(c, VSIG_E_UNSUPPORTED, "abs stats: dtype must be VSIG_DTYPE_C128 or VSIG_DTYPE_F64");
+  int rc = ensure_buf(c, &c->sscratch, &c->sscratch_bytes, vsig::np_stats_scratch_bytes(n));
+  if (rc) return rc;
+  Timed t(c, "stats");
+  HIPCHK(c, vsig::launch_np_stats(dtype, a, n, stats_dev, c->sscratch, c->stream));
+  return VSIG_OK;
+}
+
+// np.correlate(a, v, mode)'s |c| for every output in numpy's operation order
+// (refine.hip, values mode), then its mean / std as above.
+int vsig_correlate_stats_dev(vsig_ctx* c, int32_t dtype, const void* a, int64_t na, const void* v,
+                             int64_t nv, int32_t mode, double* stats_dev) {
+  if (!c || !a || !v || !stats_dev) return fail(c, VSIG_E_INVALID, "null pointer");
+  if (na < 1 || nv < 1) return fail(c, VSIG_E_INVALID, "empty input");
+  if (dtype != VSIG_DTYPE_C64 && dtype != VSIG_DTYPE_C128)
+    return fail(c, VSIG_E_INVALID, "dtype must be VSIG_DTYPE_C64 or VSIG_DTYPE_C128");
+  const long long nmin = na < nv ? na : nv, nmax = na < nv ? nv : na;
+  long long F, nout;
+  if (mode == VSIG_MODE_FULL) { F = 0; nout = na + nv - 1; }
+  else if (mode == VSIG_MODE_VALID) { F = nmin - 1; nout = nmax - nmin + 1; }
+  else if (mode == VSIG_MODE_SAME) { F = na >= nv ? nmin - 1 - nmin / 2 : nmin / 2; nout = nmax; }
+  else return fail(c, VSIG_E_INVALID, "mode must be VALID, FULL or SAME");
+  const size_t vb = ((size_t)nout * 8 + 255) & ~(size_t)255;
+  const size_t kb = (vsig::refine_values_scratch_bytes() + 255) & ~(size_t)255;
+  int rc = ensure_buf(c, &c->vscratch, &c->vscratch_bytes, vb + kb);
+  if (rc) return rc;
+  if ((rc = ensure_buf(c, &c->sscratch, &c->sscratch_bytes, vsig::np_stats_scratch_bytes(nout))))
+    return rc;
+  double* vals = static_cast<double*>(c->vscratch);
+  vsig::RefineArgs r{};
+  r.a = a; r.na = na; r.v = v; r.nv = nv; r.c128 = dtype == VSIG_DTYPE_C128;
+  r.nout = nout; r.F = F; r.waves = 1; r.Q = 1; r.rsub = 1;
+  r.blas_threads = c->blas_threads;
+  r.scratch = static_cast<char*>(c->vscratch) + vb;
+  Timed t(c, "stats");
+  HIPCHK(c, vsig::launch_refine_values(r, 0, nout - 1, vals, c->stream));
+  HIPCHK(c, vsig::launch_np_stats(VSIG_DTYPE_F64, vals, nout, stats_dev, c->sscratch, c->stream));
   return VSIG_OK;
 }
 

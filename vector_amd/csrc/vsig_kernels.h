@@ -165,13 +165,26 @@ struct RefineArgs {
   int finalize;                     // finalize the partials here (+ select, one launch):
   PeakPartial* tmp;                 //   kFinalizeTmp first-level records,
   unsigned long long* done;         //   a counter that is zero between launches
-  long long cap_items;
-  void* scratch;                    // refine_scratch_bytes(cap_items, Q)
+  long long cap;                    // opt-in limit on candidate outputs (0: none)
+  void* scratch;                    // refine_scratch_bytes(*this)
   PeakPartial* rec;                 // finalized record (max |c|), updated in place
   void* out128;                     // optional complex128 c to patch (final space)
 };
-size_t refine_scratch_bytes(long long cap_items, int Q);
+size_t refine_scratch_bytes(const RefineArgs& r);
 hipError_t launch_refine(const RefineArgs& r, hipStream_t st);
+// numpy's |c| of every output o in [lo, hi] into vals[o - lo] (operands and
+// geometry of r; scratch: refine_values_scratch_bytes()); r.rec (optional)
+// receives numpy's argmax over the range.
+size_t refine_values_scratch_bytes();
+hipError_t launch_refine_values(const RefineArgs& r, long long lo, long long hi, double* vals,
+                                hipStream_t st);
+// reduce.hip: numpy's np.mean(np.abs(a)) and np.std(np.abs(a)) (float64
+// pairwise sums over 8192-element buffers, two passes) of an array of dtype
+// VSIG_C128 or VSIG_F64 into out[0], out[1] (device); scratch:
+// np_stats_scratch_bytes(n).
+size_t np_stats_scratch_bytes(long long n);
+hipError_t launch_np_stats(int dtype, const void* a, long long n, double* out, void* scratch,
+                           hipStream_t st);
 hipError_t launch_convert_c(int to128, const void* x, long long n, void* y, hipStream_t st);
 
 // bigfft.hip: four-step FFT of M = N1 N2 > 16384 points, Bluestein for any

@@ -92,17 +92,46 @@ def _read_peak(buf: torch.Tensor):
     return float(raw[0]), idx, float(raw[2]), float(raw[3])
 
 
-def _confidence(peak, s1, s2, n, threshold_ratio):
-    """find_correlation_peak's confidence (utils.py:1328-1340) from the sums."""
-    mean = s1 / n
-    var = s2 / n - mean * mean
-    if var <= 1e-13 * (s2 / n):   # a flat |c| (std == 0 in numpy up to rounding)
-        conf = 0.0
+def _confidence_np(peak, mean, std, threshold_ratio):
+    """find_correlation_peak's confidence (utils.py:1328-1340) from numpy's
+    mean_corr / std_corr, with the reference's arithmetic."""
+    if std > 0:
+        conf = np.clip(((np.float64(peak) - mean) / std) / 10.0, 0.0, 1.0)
     else:
-        conf = float(np.clip((peak - mean) / np.sqrt(var) / 10.0, 0.0, 1.0))
+        conf = 0.0
     if peak < threshold_ratio * peak:   # utils.py:1339: peak == max(|c|)
         conf = 0.0
     return conf
+
+
+# The fused correlators sum fp32 |c| values (errors ~1e-6 of the peak); below
+# this spread (std / peak) their single-pass variance no longer resolves
+# numpy's, and the statistics are recomputed from numpy-order values
+# (vsig_correlate_stats_dev) -- a flat |c| (a tone) has a std of rounding noise.
+_FUSED_STD_FLOOR = 1e-3
+
+
+def _fused_stats(peak, s1, s2, n):
+    """(mean, std, resolved) from the fused record's sums."""
+    mean = s1 / n
+    var = s2 / n - mean * mean
+    std = float(np.sqrt(var)) if var > 0 else 0.0
+    return mean, std, std > _FUSED_STD_FLOOR * peak
+
+
+def _confidence(peak, s1, s2, n, threshold_ratio):
+    """The confidence from a fused record's sums (single pass; see _FUSED_STD_FLOOR)."""
+    mean, std, _ = _fused_stats(peak, s1, s2, n)
+    return _confidence_np(peak, mean, std, threshold_ratio)
+
+
+def _abs_stats(t: torch.Tensor, code: str, ctx):
+    """numpy's (np.mean, np.std) of |t| on the GPU (vsig_abs_stats_dev)."""
+    out = torch.empty(2, dtype=torch.float64, device=t.device)
+    ctx.check(ctx.lib.vsig_abs_stats_dev(ctx.h, _lib.DTYPES[code], _ptr(t), int(t.numel()), _ptr(out)),
+              "abs stats")
+    m, sd = out.cpu().tolist()
+    return np.float64(m), np.float64(sd)
 
 
 # ---------------------------------------------------------------------------
@@ -369,6 +398,7 @@ def _correlate_dev(a, v, mode, want_array, ctx, out128=False):
     in128 = _is_c128(a) or _is_c128(v)
     conv = _device_c128 if in128 else _device_c64
     ad, vd = conv(a, ctx), conv(v, ctx)
+    ctx.sync_blas_threads()
     na, nv = int(ad.shape[0]), int(vd.shape[0])
     if na == 0:
         raise ValueError("a cannot be empty")
@@ -383,13 +413,13 @@ def _correlate_dev(a, v, mode, want_array, ctx, out128=False):
                                          _lib.DTYPES["c128" if out128 else "c64"],
                                          _ptr(c) if c is not None else None, _ptr(pk)),
               "correlate")
-    return c, pk, nout
+    return c, pk, nout, (ad, vd, in128)
 
 
 def refine_status(ctx=None):
     """(status, candidates) of the last correlation's argmax refine:
-    0 refined, 1 skipped (more candidates than the 'refine_cap' option),
-    2 no refine pass ran."""
+    0 refined, 1 skipped (more candidate outputs than a 'refine_cap' option
+    set > 0; the default is no limit), 2 no refine pass ran."""
     ctx = ctx or _lib.get_context()
     st, nc = C.c_int32(), C.c_int64()
     ctx.check(ctx.lib.vsig_refine_status(ctx.h, C.byref(st), C.byref(nc)), "refine_status")
@@ -399,8 +429,8 @@ def refine_status(ctx=None):
 def _warn_unrefined(ctx):
     st, nc = refine_status(ctx)
     if st == 1:
-        warnings.warn(f"correlation argmax left at fp32 accuracy: {nc} candidate waves within the "
-                      f"refine band exceed the 'refine_cap' option", RuntimeWarning, stacklevel=3)
+        warnings.warn(f"correlation argmax left at fp32 accuracy: the {nc} candidate items within "
+                      f"the refine band exceed the 'refine_cap' option", RuntimeWarning, stacklevel=3)
 
 
 def cross_correlate_signals(signal1, signal2, mode="full"):
@@ -413,7 +443,7 @@ def cross_correlate_signals(signal1, signal2, mode="full"):
     ctx = _lib.get_context()
     dev = _is_dev(signal1) or _is_dev(signal2)
     out128 = (not dev) or _is_c128(signal1) or _is_c128(signal2)
-    c, _, _ = _correlate_dev(signal2, signal1, mode, True, ctx, out128=out128)
+    c, _, _, _ = _correlate_dev(signal2, signal1, mode, True, ctx, out128=out128)
     l1 = int(signal1.shape[0]) if _is_dev(signal1) else len(signal1)
     l2 = int(signal2.shape[0]) if _is_dev(signal2) else len(signal2)
     lags = _lags(mode, l1, l2)
@@ -427,10 +457,8 @@ def cross_correlate_signals(signal1, signal2, mode="full"):
 correlate = cross_correlate_signals
 
 
-def peak_stats(a):
-    """(argmax of |a| (first), max |a|, sum |a|, sum |a|^2, n) in double
-    precision on the GPU, for numpy or CUDA arrays of complex/real dtype."""
-    ctx = _lib.get_context()
+def _stats_operand(a, ctx):
+    """a as a contiguous CUDA tensor and its dtype code."""
     if _is_dev(a):
         t = a.contiguous()
         code = {torch.complex128: "c128", torch.complex64: "c64", torch.float64: "f64",
@@ -450,6 +478,14 @@ def peak_stats(a):
         else:
             arr, code = arr.astype(np.float64), "f64"
         t = torch.from_numpy(np.ascontiguousarray(arr.ravel())).to(f"cuda:{ctx.device}")
+    return t, code
+
+
+def peak_stats(a):
+    """(argmax of |a| (first), max |a|, sum |a|, sum |a|^2, n) in double
+    precision on the GPU, for numpy or CUDA arrays of complex/real dtype."""
+    ctx = _lib.get_context()
+    t, code = _stats_operand(a, ctx)
     n = int(t.numel())
     if n == 0:
         raise ValueError("attempt to get argmax of an empty sequence")
@@ -460,10 +496,23 @@ def peak_stats(a):
 
 
 def find_correlation_peak(correlation, lags, threshold_ratio=0.5):
-    """utils.py:1298-1342 — (lags[argmax |c|], max |c|, confidence)."""
-    idx, peak, s1, s2, n = peak_stats(correlation)
-    conf = _confidence(peak, s1, s2, n, threshold_ratio)
-    return lags[idx], np.float64(peak), conf
+    """utils.py:1298-1342 — (lags[argmax |c|], max |c|, confidence).
+    complex128 / float64 arrays (cross_correlate_signals' output): mean and std
+    of |c| exactly as numpy forms them (its pairwise sums, two passes); other
+    dtypes: from double sums of |c| (single pass)."""
+    ctx = _lib.get_context()
+    t, code = _stats_operand(correlation, ctx)
+    n = int(t.numel())
+    if n == 0:
+        raise ValueError("attempt to get argmax of an empty sequence")
+    pk = _peak_buffer(ctx)
+    ctx.check(ctx.lib.vsig_peak_dev(ctx.h, _lib.DTYPES[code], _ptr(t), n, _ptr(pk)), "peak")
+    peak, idx, s1, s2 = _read_peak(pk)
+    if code in ("c128", "f64"):
+        mean, std = _abs_stats(t, code, ctx)
+    else:
+        mean, std, _ = _fused_stats(peak, s1, s2, n)
+    return lags[idx], np.float64(peak), _confidence_np(peak, mean, std, threshold_ratio)
 
 
 def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
@@ -471,9 +520,19 @@ def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
     fused: the correlation is reduced inside the kernel and never stored."""
     _check_mode(mode)
     ctx = _lib.get_context()
-    _, pk, nout = _correlate_dev(signal2, signal1, mode, False, ctx)
+    _, pk, nout, (ad, vd, in128) = _correlate_dev(signal2, signal1, mode, False, ctx)
     peak, idx, s1, s2 = _read_peak(pk)
     _warn_unrefined(ctx)
+    mean, std, resolved = _fused_stats(peak, s1, s2, nout)
+    if not resolved:
+        # a (nearly) flat |c|: numpy's std is decided by rounding; every
+        # output's |c| in numpy's order, then numpy's two-pass statistics
+        st = torch.empty(2, dtype=torch.float64, device=ad.device)
+        ctx.check(ctx.lib.vsig_correlate_stats_dev(
+            ctx.h, _lib.DTYPES["c128" if in128 else "c64"], _ptr(ad), int(ad.shape[0]), _ptr(vd),
+            int(vd.shape[0]), _lib.MODES[mode], _ptr(st)), "correlate stats")
+        mean, std = (np.float64(x) for x in st.cpu().tolist())
+    conf = _confidence_np(peak, mean, std, threshold_ratio)
     l1 = int(signal1.shape[0]) if _is_dev(signal1) else len(signal1)
     l2 = int(signal2.shape[0]) if _is_dev(signal2) else len(signal2)
     if mode == "full":
@@ -485,7 +544,7 @@ def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
         lag = np.int64(idx)
     else:
         lag = _lags(mode, l1, l2)[idx]      # raises IndexError like the reference
-    return lag, np.float64(peak), _confidence(peak, s1, s2, nout, threshold_ratio)
+    return lag, np.float64(peak), conf
 
 
 class Correlator:
