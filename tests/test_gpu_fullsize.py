@@ -124,3 +124,41 @@ def test_c3_sync_2pow30(gpu):
     assert s2 == pytest.approx(float((a * a).sum()), rel=1e-5)
     del c, a, x
     torch.cuda.empty_cache()
+
+
+def test_c4_pfb_per_gpu_full_shape(gpu):
+    """BASELINE config 4's per-GPU shape: the 64-channel, 16-branch PFB
+    (prototype firwin(1024, 1/64), bench.py run_pfb) over 2**29 device-resident
+    samples (config 4's 2**31 over 4 GPUs).  Frames at sampled positions (first,
+    middle, last, in both walk directions of the kernel's lane groups) against
+    the oracle's definition on those input slices, and a tone planted at
+    channel 5's centre over the last quarter of the capture lands in channel 5."""
+    import scipy.signal
+    b = _bench()
+    C, P, n = 64, 16, 1 << 29
+    proto = scipy.signal.firwin(P * C, 1.0 / C).astype(np.float32)
+    x = torch.empty(n, dtype=torch.complex64, device="cuda")
+    b.generate_chunk(x, 0, 4242, np.zeros(0, np.complex64), -1)
+    q0 = 3 * n // 4
+    idx = torch.arange(q0, n, device="cuda", dtype=torch.float64)
+    ph = torch.remainder(idx * (5.0 / C), 1.0) * (2 * np.pi)
+    x[q0:] += (8.0 * torch.polar(torch.ones_like(ph), ph)).to(torch.complex64)
+    del idx, ph
+    ch = gpu.Channelizer(proto, C)
+    M = ch.nframes(n)
+    out = torch.empty((M, C), dtype=torch.complex64, device="cuda")
+    ch(x, out=out)
+    torch.cuda.synchronize()
+    for m0 in (0, 63, 64, 4097, M // 2 - 5, q0 // C + 100, M - 70, M - 8):
+        K = 8
+        K = min(K, M - m0)
+        xs = x[m0 * C: (m0 + K - 1) * C + P * C].cpu().numpy()
+        want = ref.pfb_channelize(xs, proto, C).T                 # (K, C)
+        got = out[m0: m0 + K].cpu().numpy()
+        assert np.abs(got - want).max() <= 1e-5 * np.abs(want).max(), m0
+    # the tone: channel 5 holds nearly all the power of the frames inside it
+    tail = out[q0 // C + P: q0 // C + P + 4096].abs().pow(2).double().sum(dim=0).cpu().numpy()
+    assert int(np.argmax(tail)) == 5
+    assert tail[5] > 0.9 * tail.sum()
+    del out, x
+    torch.cuda.empty_cache()

@@ -294,7 +294,7 @@ def find_packet_start(signal, template=None, threshold_ratio=0.2, window_size=No
         ta = torch.empty(int(tm.numel()), dtype=odt, device=s.device)
         ctx.check(absfn(ctx.h, _lib.DTYPES[scode], _ptr(s), int(s.numel()), _ptr(sa)), "abs")
         ctx.check(absfn(ctx.h, _lib.DTYPES[tcode], _ptr(tm), int(tm.numel()), _ptr(ta)), "abs")
-        _, pk, _ = _correlate_dev(sa, ta, "valid", False, ctx)
+        _, pk, _, _ = _correlate_dev(sa, ta, "valid", False, ctx)
         return int(pk.cpu().view(torch.int64)[1].item())
     t, code = _to_device(signal, ctx)
     n = int(t.numel())

@@ -356,7 +356,9 @@ int vsig_rccl_transport(void* comm, vsig_transport* out) {
 // In-process loopback transport: the ranks are host threads of one process
 // (one vsig_ctx / stream each, any devices with peer access).  A send posts
 // its buffer and an event recorded after it on the sender's stream; the
-// receiver waits for the post, makes its stream wait on the event and copies.
+// receiver waits for the post, makes its stream wait on the event and copies;
+// sendrecv returns once its own post has been copied (blocking, as
+// MPI_Sendrecv: the sender's next kernels may overwrite the buffer).
 // ---------------------------------------------------------------------------
 struct vsig_loopback {
   int world = 0;
@@ -407,6 +409,13 @@ int loop_sendrecv(void* user, const void* send, int64_t sb, int32_t dst, void* r
     std::unique_lock<std::mutex> lk(lb->mu);
     lb->box[src * W + lr->rank].full = false;
     lb->cv.notify_all();
+  }
+  if (send && dst >= 0) {
+    // like MPI_Sendrecv: return once the receiver has copied our buffer (the
+    // caller's later kernels may overwrite it)
+    std::unique_lock<std::mutex> lk(lb->mu);
+    auto& b = lb->box[lr->rank * W + dst];
+    lb->cv.wait(lk, [&] { return !b.full; });
   }
   return 0;
 }

@@ -20,8 +20,12 @@ and the 32-byte peak records cross xGMI.  Reference precedent: the overlapped
 chunking of heavy_packet_optimizer.py:114-152 (whose merge duplicated the
 overlap, :195-222 — not reproduced here).
 
-The compute steps go through a backend object so the orchestration can be
-unit-tested on CPU with gloo; the product backend is HipBackend (libvsig.so).
+The compute steps go through a backend object and the exchanges through a
+transport object, so that the same orchestration runs in production (HipBackend
+on libvsig.so, TorchTransport = torch.distributed over RCCL), on CPU under gloo
+(tests/test_shard_gloo.py) and as several ranks in one process on one GPU
+(HipBackend + NativeTransport over the library's loopback,
+tests/test_gpu_shard_threads.py).
 """
 from __future__ import annotations
 
@@ -32,7 +36,7 @@ import torch
 import torch.distributed as dist
 
 __all__ = ["ChainConfig", "HipBackend", "StreamChain", "combine_peaks", "HipPfbBackend",
-           "PfbChain", "NativeChain", "Loopback"]
+           "PfbChain", "NativeChain", "Loopback", "TorchTransport", "NativeTransport"]
 
 
 @dataclass
@@ -70,6 +74,70 @@ def combine_peaks(rows: np.ndarray) -> tuple[float, int, float, float]:
         s1 += float(a)
         s2 += float(b)
     return best[0], best[1], s1, s2
+
+
+class TorchTransport:
+    """Exchanges over torch.distributed (production: backend 'nccl' = RCCL over
+    xGMI; gloo on CPU): non-blocking point-to-point halos and an asynchronous
+    all-gather, each returning handles for wait()."""
+
+    def __init__(self, group=None):
+        self.group = group
+
+    def exchange_start(self, send, dst, recv, src):
+        ops = []
+        if send is not None and dst is not None:
+            ops.append(dist.P2POp(dist.isend, send, dst, group=self.group))
+        if recv is not None and src is not None:
+            ops.append(dist.P2POp(dist.irecv, recv, src, group=self.group))
+        return dist.batch_isend_irecv(ops) if ops else []
+
+    def all_gather_start(self, rows, rec):
+        return [dist.all_gather_into_tensor(rows, rec, group=self.group, async_op=True)]
+
+    @staticmethod
+    def wait(handles):
+        for h in handles or ():
+            h.wait()
+
+
+class NativeTransport:
+    """Exchanges through a C vsig_transport (include/vsig.h): the library's
+    in-process Loopback (ranks as threads of one process, e.g. several ranks on
+    one GPU) or its RCCL transport.  Blocking sendrecv / allgather ordered on
+    torch's current stream (the call returns once the partner has the data;
+    ctypes releases the GIL around it, so rank threads proceed in parallel)."""
+
+    def __init__(self, t):
+        self.t = t
+
+    @staticmethod
+    def _ptr_bytes(x):
+        return (x.data_ptr(), x.numel() * x.element_size()) if x is not None else (None, 0)
+
+    def exchange_start(self, send, dst, recv, src):
+        sp, sb = self._ptr_bytes(send if dst is not None else None)
+        rp, rb = self._ptr_bytes(recv if src is not None else None)
+        if sp is None and rp is None:
+            return []
+        st = torch.cuda.current_stream().cuda_stream
+        rc = self.t.sendrecv(self.t.user, sp, sb, -1 if sp is None else int(dst), rp, rb,
+                             -1 if rp is None else int(src), st)
+        if rc:
+            raise RuntimeError(f"transport sendrecv failed ({rc})")
+        return []
+
+    def all_gather_start(self, rows, rec):
+        st = torch.cuda.current_stream().cuda_stream
+        rc = self.t.allgather(self.t.user, rec.data_ptr(), rows.data_ptr(),
+                              rec.numel() * rec.element_size(), st)
+        if rc:
+            raise RuntimeError(f"transport allgather failed ({rc})")
+        return []
+
+    @staticmethod
+    def wait(handles):
+        pass
 
 
 class HipBackend:
@@ -118,9 +186,11 @@ class HipBackend:
 class StreamChain:
     """One rank's part of the sharded chain (world = 1: the plain chain)."""
 
-    def __init__(self, cfg: ChainConfig, backend, rank: int = 0, world: int = 1, group=None):
+    def __init__(self, cfg: ChainConfig, backend, rank: int = 0, world: int = 1, group=None,
+                 transport=None):
         cfg.validate(world)
         self.cfg, self.be, self.rank, self.world, self.group = cfg, backend, rank, world, group
+        self.tr = transport if transport is not None else TorchTransport(group)
         self.hist = len(cfg.taps) - 1
         self.ny = cfg.n_local // cfg.decim
         self.L = len(cfg.template) if cfg.template is not None else 0
@@ -154,27 +224,18 @@ class StreamChain:
     def _begin_step(self):
         self._slot ^= 1
         work, self._gather[self._slot] = self._gather[self._slot], None
-        if work is not None:              # the all-gather two steps back (long done)
-            work.wait()
+        self.tr.wait(work)                # the all-gather two steps back (long done)
 
     def _gather_peaks(self):
         rows = self._rows[self._slot]
-        self._gather[self._slot] = dist.all_gather_into_tensor(rows, self.rec, group=self.group,
-                                                               async_op=True)
+        self._gather[self._slot] = self.tr.all_gather_start(rows, self.rec)
         return list(rows.view(self.world, 4).unbind(0))
 
     def _exchange_start(self, send, dst, recv, src):
-        ops = []
-        if send is not None and dst is not None:
-            ops.append(dist.P2POp(dist.isend, send, dst, group=self.group))
-        if recv is not None and src is not None:
-            ops.append(dist.P2POp(dist.irecv, recv, src, group=self.group))
-        return dist.batch_isend_irecv(ops) if ops else []
+        return self.tr.exchange_start(send, dst, recv, src)
 
-    @staticmethod
-    def _exchange_wait(reqs):
-        for req in reqs:
-            req.wait()
+    def _exchange_wait(self, reqs):
+        self.tr.wait(reqs)
 
     def _exchange(self, send, dst, recv, src):
         self._exchange_wait(self._exchange_start(send, dst, recv, src))
@@ -236,9 +297,7 @@ class StreamChain:
 
     def global_peak(self):
         """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step."""
-        work = self._gather[self._slot]
-        if work is not None:
-            work.wait()
+        self.tr.wait(self._gather[self._slot])
         rows = []
         for r, t in enumerate(self.peak_rows):
             h = t.detach().cpu().reshape(4)
@@ -393,7 +452,7 @@ class PfbChain:
     single-stream result exactly ((world*n - ntaps)//C + 1 frames)."""
 
     def __init__(self, n_local: int, proto, nchan: int, backend, rank: int = 0, world: int = 1,
-                 group=None):
+                 group=None, transport=None):
         C, ntaps = int(nchan), len(proto)
         if n_local % C:
             raise ValueError("n_local must be a multiple of nchan (frames never straddle ranks)")
@@ -401,6 +460,7 @@ class PfbChain:
             raise ValueError("chunk shorter than the PFB halo")
         self.n, self.C, self.ntaps = n_local, C, ntaps
         self.be, self.rank, self.world, self.group = backend, rank, world, group
+        self.tr = transport if transport is not None else TorchTransport(group)
         self.halo = ntaps - C
         self.rhalo = self.halo if rank < world - 1 else 0
         self.nframes = n_local // C if rank < world - 1 else max(0, (n_local - ntaps) // C + 1)
@@ -419,14 +479,10 @@ class PfbChain:
     def step(self):
         r, w, h = self.rank, self.world, self.halo
         if w > 1 and h > 0:
-            ops = []
-            if r > 0:
-                ops.append(dist.P2POp(dist.isend, self.x_ext[:h], r - 1, group=self.group))
-            if r < w - 1:
-                ops.append(dist.P2POp(dist.irecv, self.x_ext[self.n: self.n + h], r + 1,
-                                      group=self.group))
-            for req in dist.batch_isend_irecv(ops):
-                req.wait()
+            self.tr.wait(self.tr.exchange_start(self.x_ext[:h] if r > 0 else None,
+                                                r - 1 if r > 0 else None,
+                                                self.x_ext[self.n: self.n + h] if r < w - 1 else None,
+                                                r + 1 if r < w - 1 else None))
         if self.nframes > 0:
             self.be.pfb_into(self.x_ext[: self.n + self.rhalo], self.y)
 
