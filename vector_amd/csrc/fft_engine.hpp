@@ -34,14 +34,11 @@ namespace vsig {
 // the scalar rate, so a complex value in an (even-aligned) VGPR pair costs one
 // instruction per add and two per multiply when the operand swizzles go into
 // the VOP3P op_sel / neg modifiers — which the compiler does not do on its own
-// for swizzled operands, hence the inline asm below.  Build with
-// -DVSIG_SCALAR_FFT for the plain two-lane scalar form (A/B reference).
+// for swizzled operands, hence the inline asm below.
 typedef float f2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ f2v tov(float2 a) { return (f2v){a.x, a.y}; }
 __device__ __forceinline__ float2 fromv(f2v a) { return make_float2(a.x, a.y); }
 
-#ifndef VSIG_SCALAR_FFT
-#define VSIG_PK 1
 __device__ __forceinline__ float2 cadd(float2 a, float2 b) { return fromv(tov(a) + tov(b)); }
 __device__ __forceinline__ float2 csub(float2 a, float2 b) { return fromv(tov(a) - tov(b)); }
 // a * b = b.x * (a.x, a.y) + b.y * (-a.y, a.x)
@@ -90,21 +87,6 @@ __device__ __forceinline__ float2 cmul_cs(float2 b, float c, float s_) {
       : "=v"(r) : "v"(bv), "s"(ss), "v"(t));
   return fromv(r);
 }
-#else
-__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
-  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ float2 cadd_mi(float2 a, float2 b) { return make_float2(a.x + b.y, a.y - b.x); }
-__device__ __forceinline__ float2 csub_mi(float2 a, float2 b) { return make_float2(a.x - b.y, a.y + b.x); }
-__device__ __forceinline__ float2 cfma_s(float2 u, float h, float2 a) {
-  return make_float2(fmaf(h, u.x, a.x), fmaf(h, u.y, a.y));
-}
-__device__ __forceinline__ float2 cmul_cs(float2 b, float c, float s_) {
-  return make_float2(b.x * c + b.y * s_, b.y * c - b.x * s_);
-}
-#endif
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
 
 // cos / sin of 2*pi*k/64, k = 0..31 (enough for every in-register radix <= 64).
@@ -161,7 +143,6 @@ __device__ __forceinline__ float2 twc(float2 b) {
 // and its consumer are never adjacent: gfx950 needs one wait state between a
 // packed fp32 op and a dependent one, and hipcc pads every inline-asm
 // boundary with one, while independent work in between costs nothing.
-#ifndef VSIG_FFT_UNPHASED
 template <int R, int P>
 struct Radix2Phased {
   static constexpr int Ns = 1 << P, M = 2 * Ns;
@@ -179,11 +160,7 @@ struct Radix2Phased {
       const float2 b = a[J + R / 2];
       if constexpr (general<J>()) {
         constexpr int idx = k * (64 / M);
-#ifdef VSIG_PK
         u[J] = fromv(tov(b) * (f2v){kCos64[idx], kCos64[idx]});
-#else
-        u[J] = b;
-#endif
       } else if constexpr (8 * k == M) {
         u[J] = cadd_mi(b, b);
       } else if constexpr (8 * k == 3 * M) {
@@ -196,15 +173,11 @@ struct Radix2Phased {
       if constexpr (general<J>()) {
         constexpr int idx = kk<J>() * (64 / M);
         const float2 b = a[J + R / 2];
-#ifdef VSIG_PK
         const f2v bv = tov(b), ss = (f2v){kSin64[idx], kSin64[idx]};
         f2v r;
         asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
             : "=v"(r) : "v"(bv), "s"(ss), "v"(tov(u[J])));
         u[J] = fromv(r);
-#else
-        u[J] = cmul_cs(b, kCos64[idx], kSin64[idx]);
-#endif
       }
     });
     // (C) the butterflies' sums
@@ -235,7 +208,6 @@ struct Radix2Phased {
     });
   }
 };
-#endif
 
 template <int R, int P, int J>
 struct Radix2Step {
@@ -275,11 +247,7 @@ template <int R, int P>
 struct DftPasses {
   __device__ __forceinline__ static void run(float2* v) {
     float2 t[R];
-#ifndef VSIG_FFT_UNPHASED
     Radix2Phased<R, P>::run(v, t);
-#else
-    Radix2Step<R, P, 0>::run(v, t);
-#endif
 #pragma unroll
     for (int i = 0; i < R; ++i) v[i] = t[i];
     if constexpr ((2 << P) < R) DftPasses<R, P + 1>::run(v);
@@ -470,9 +438,6 @@ struct wave_sync_of<P, decltype(void(P::WAVE_SYNC))> { static constexpr bool val
 
 template <class P>
 __device__ __forceinline__ void plan_sync() {
-#ifdef VSIG_KO_NOBAR      // tuning knock-out (results wrong): no exchange barriers
-  return;
-#endif
   if constexpr (wave_sync_of<P>::value) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -626,7 +591,6 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
     const float2* wa = tws.wa + anch_off<P>(p) + (anch_nb<P>(p) == 1 ? 0 : b) * NA;
     const float2 w1 = wa[0];
     float2 cur = w1;
-#if defined(VSIG_PK) && !defined(VSIG_FFT_UNPHASED)
     // software-pipelined by one power: the next power's product and this
     // element's product alternate, so no packed op is followed by its
     // dependent (one wait state each otherwise, see Radix2Phased)
@@ -642,13 +606,6 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
       v[b * R + r] = cmul_fin(v[b * R + r], cur, tv);
       cur = nxt;
     });
-#else
-#pragma unroll
-    for (int r = 1; r < R; ++r) {
-      if (r > 1) cur = (r % 8 == 0) ? wa[r / 8] : cmul(cur, w1);
-      v[b * R + r] = cmul(v[b * R + r], cur);
-    }
-#endif
   }
 }
 
@@ -707,9 +664,6 @@ __device__ __forceinline__ int store_base(int j) {
 
 template <class P, int p>
 __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
-#ifdef VSIG_KO_NOLDS      // tuning knock-out (results wrong): no exchange traffic
-  if constexpr (true) return;
-#endif
   constexpr int R = P::R[p];
   constexpr int Ns = P::ns(p);
   constexpr int B = P::E / R;
@@ -727,13 +681,6 @@ __device__ __forceinline__ void fft_store(const float2* v, float2* lds, int t) {
 
 template <class P, int p>
 __device__ __forceinline__ void fft_load(float2* v, const float2* lds, int t) {
-#ifdef VSIG_KO_NOLDS
-  if constexpr (true) {     // keep v opaque so the passes are not folded
-#pragma unroll
-    for (int i = 0; i < P::E; ++i) asm volatile("" : "+v"(v[i].x), "+v"(v[i].y));
-    return;
-  }
-#endif
   constexpr int R = P::R[p];
   constexpr int B = P::E / R;
   if constexpr (pass_map<P, p>() == kMapIlv) {
@@ -981,13 +928,11 @@ using Plan256d = Plan<256, 4, 4, 4, 4, 4>;
 // FIR wave, = SQ_LDS_BANK_CONFLICT / wave of the D = 4 FIR); 4 pads per 16
 // spread them over all 32 banks.  Exchanges 1 and 3 are conflict-free as they
 // are (tools/ldssim.py models every exchange of fir_poly_kernel / fir_dec_kernel).
-#ifndef VSIG_NO_XPAD      // tuning builds: round 2's uniform padding
 template <>
 struct xpad<Plan256d, 2> {
   static constexpr int S = 4;
   static constexpr int U = 2;
 };
-#endif
 // Polyphase front of the D = 4 decimating FIR: the two radix-16 passes of a
 // 1024-point transform = the 256-point spectra of its 4 polyphase components
 // (pass-1 twiddles = Plan256's table).
@@ -1000,13 +945,11 @@ using Plan1024x = Lanes<Plan1024s, kMapPair, kMapPair>;
 // 32 (2-way: 256 extra LDS cycles per D = 1 FIR wave, = the c2 PMC's
 // SQ_LDS_BANK_CONFLICT / wave); 1 pad per 16 there is conflict-free for both
 // sides (tools/ldssim.py).
-#ifndef VSIG_NO_XPAD
 template <>
 struct xpad<Plan1024x, 2> {
   static constexpr int S = 4;
   static constexpr int U = 0;
 };
-#endif
 // The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
 using Plan8192x = Swz<Plan8192>;
 // The same size on 512 threads x 16 values (four passes, the radix-2 one with
@@ -1015,21 +958,15 @@ using Plan8192x = Swz<Plan8192>;
 using Plan8192w = Swz<Plan<8192, 16, 16, 2, 16, 16>>;
 // The PSD's 8192-point plan with interleaved first / last passes (16-byte
 // frame loads, 8-byte |X|^2 stores, conflict-free exchanges).
-#ifndef VSIG_ILV_S            // tuning builds: the interleaved plan's padding
-#define VSIG_ILV_S 5
-#define VSIG_ILV_U 1
-#endif
-using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, VSIG_ILV_S, VSIG_ILV_U>;
+using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, 5, 1>;
 // Its second exchange's 16-byte pair reads (2t + 512 r: ds_read_b128 lane groups
 // of 16) meet 2-way on banks under 2 pads per 32; 2 pads per 64 spreads them
 // (tools/ldssim.py: 64 extra LDS cycles per wave and frame -> 0).
-#ifndef VSIG_NO_XPAD
 template <>
 struct xpad<Plan8192i, 2> {
   static constexpr int S = 6;
   static constexpr int U = 1;
 };
-#endif
 
 template <class P>
 constexpr int block_threads() { return P::TF > 256 ? P::TF : 256; }

@@ -100,9 +100,7 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     load_segment<P>(d, x, g0 + b1 * hop - lo, n, t);
   }
   launder_anchors<P>(wa);
-#ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
-#endif
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const float2 h = Hs[out_index<P>(t, e)];
@@ -110,9 +108,7 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     d[e] = cconj(cmul(d[e], h));
   }
   launder_anchors<P>(wa);
-#ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
-#endif
   if constexpr (XS) {
     fir_store_x4<P>(a, y, b0, hop, lo, nloc, t);
     fir_store_x4<P>(d, y, b1, hop, lo, nloc, t);
@@ -221,12 +217,12 @@ __device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
               make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
 }
 
-// Tuning builds: VSIG_FIR_KO skips both transform pairs (memory-only
-// knock-out, outputs wrong): 3.85-3.94 ms at config 5 against 4.32-4.37 ms
-// for the kernel (profiles/r02_v12_ab.txt), i.e. the loads / stores of this
-// access pattern alone run at 5.5 TB/s and the transforms add ~0.45 ms.
+// A memory-only knock-out of this kernel (both transform pairs skipped,
+// outputs wrong; round 2): 3.85-3.94 ms at config 5 against 4.32-4.37 ms
+// for the kernel then (profiles/r02_v12_ab.txt), i.e. the loads / stores of
+// this access pattern alone run at 5.5 TB/s and the transforms add ~0.45 ms.
 
-template <bool MIX = false, bool X4 = false, bool PERSIST = false>
+template <bool MIX = false, bool X4 = false>
 __global__ __launch_bounds__(64) void fir_poly_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
     long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
@@ -245,14 +241,9 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
   load_anchors<P>(wa, tw, t0);
   float2 wr[rtw_total<PD>()];
   load_rtw<PD>(wr, twd, tq0);
-  // PERSIST (tuning builds, VSIG_TUNING): a fixed grid walks the segment pairs
-  // (grid-stride), so that a bounded number of waves is resident; the thread
-  // index is opaque per iteration (no hoisted, pinned per-element addresses)
-  for (long long it = PERSIST ? blockIdx.x : 0;; it += gridDim.x) {
-  const long long b = PERSIST ? it : xcd_remap(blockIdx.x, gridDim.x);
+  const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (2 * b >= nblocks) return;
-  const int zz = PERSIST ? opaque_zero() : 0;
-  const int t = t0 + zz, tq = tq0 + zz;
+  const int t = t0, tq = tq0;
   float2 a[P::E], d[P::E];
   if constexpr (MIX) {
     load_segment_mix<P>(a, x, g0 + (2 * b) * hop - lo2, n, t, mix);
@@ -264,31 +255,19 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
     load_segment<P>(d, x, g0 + (2 * b + 1) * hop - lo2, n, t);
   }
   launder_anchors<P>(wa);
-#ifndef VSIG_FIR_KO
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
-#endif
-#ifndef VSIG_NO_GLANE
   // lane-major G (fir_poly_gtable): load r gives lane t its G(t, 2r), G(t, 2r + 1)
   const float4* G4 = reinterpret_cast<const float4*>(G) + t;
-#else
-  const float2* Gk = G + (t >> 4) * 256 + (t & 15);
-#endif
   float2 ua[PD::E], ud[PD::E];
 #pragma unroll
   for (int i = 0; i < PD::E; ++i) {
     float2 pa[4], pd[4];
-#ifndef VSIG_NO_GLANE
     const float4 g01 = G4[64 * (2 * i)], g23 = G4[64 * (2 * i + 1)];
     const float2 gq[4] = {make_float2(g01.x, g01.y), make_float2(g01.z, g01.w),
                           make_float2(g23.x, g23.y), make_float2(g23.z, g23.w)};
-#endif
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-#ifndef VSIG_NO_GLANE
       const float2 g = gq[q];
-#else
-      const float2 g = Gk[16 * (4 * i + q)];
-#endif
       pa[q] = cmul(a[4 * i + q], g);
       pd[q] = cmul(d[4 * i + q], g);
     }
@@ -297,9 +276,7 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
     ua[i] = cconj(swap16_add(sa0, sa1));
     ud[i] = cconj(swap16_add(sd0, sd1));
   }
-#ifndef VSIG_FIR_KO
   fft_pair<PD>(ua, ud, lds, TwRegs{wr}, tq);
-#endif
   const int n0 = lo2 / D, n1 = (lo2 + (int)hop) / D;
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
@@ -312,8 +289,6 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
       const int i = out_index<PD>(tq, e);
       if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, cconj(u[e]));
     }
-  }
-  if constexpr (!PERSIST) return;
   }
 }
 
@@ -330,14 +305,10 @@ __global__ void fir_poly_gtable(const float2* __restrict__ Hs, float2* __restric
     re += (double)h.x * cs - (double)h.y * sn;
     im += (double)h.x * sn + (double)h.y * cs;
   }
-#ifndef VSIG_NO_GLANE
   // lane-major: lane t = 16 k + (j & 15) uses G(t, m), m = j >> 4, from its
   // float4 m >> 1 (fir_poly_kernel)
   const int t = (k << 4) | (j & 15), m = j >> 4;
   G[((m >> 1) * 64 + t) * 2 + (m & 1)] = make_float2((float)re, (float)im);
-#else
-  G[i] = make_float2((float)re, (float)im);
-#endif
 }
 
 hipError_t launch_fir_poly_gtable(const float2* Hs, float2* G, hipStream_t st) {
@@ -348,9 +319,6 @@ hipError_t launch_fir_poly_gtable(const float2* Hs, float2* G, hipStream_t st) {
 // Every segment start x + off + k hop (k >= 0) 16-byte aligned: the 16-byte
 // segment loads (load_segment_x4) apply.
 static bool x4_aligned(const float2* x, long long off, long long hop) {
-#ifdef VSIG_NO_X4       // tuning builds: 8-byte segment loads only
-  return false;
-#endif
   return (hop % 2) == 0 && ((reinterpret_cast<uintptr_t>(x) + 8 * (uintptr_t)off) & 15) == 0;
 }
 
@@ -363,11 +331,6 @@ hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const flo
   const MixArgs m = mix ? *mix : MixArgs{};
   if (mix)
     hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
-#ifdef VSIG_TUNING
-  else if (g_tune_fir_grid > 0 && x4_aligned(x, g0 - lo2, hop))
-    hipLaunchKernelGGL((fir_poly_kernel<false, true, true>), dim3((unsigned)g_tune_fir_grid), blk, 0, st, x,
-                       n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
-#endif
   else if (x4_aligned(x, g0 - lo2, hop))
     hipLaunchKernelGGL((fir_poly_kernel<false, true>), g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw,
                        twd, m);
@@ -416,11 +379,7 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
       }
     }
     if constexpr (map0_of<PL>::value == kMapPair) {
-#ifdef VSIG_NO_XS      // tuning builds: 8-byte stores
-      const bool xs = false;
-#else
       const bool xs = decim == 1 && (ntaps - 1) % 2 == 0 && x4_aligned(y, 0, hop);
-#endif
       if (x4_aligned(x, g0 - (ntaps - 1), hop)) {
         if (xs)
           hipLaunchKernelGGL((fir_os_kernel<PL, false, true, true>), grid, dim3(PL::TF), 0, st, x, n, g0,

@@ -107,7 +107,6 @@ __device__ __forceinline__ void load_pair_x4(float2* a, float2* d, const float2*
                                              long long s0, long long hop, long long n, int t) {
   static_assert(map0_of<P>::value == kMapPair && P::TF == 64 && P::E == 16 && P::R[0] == 16,
                 "operand layout m(t) + 64 e");
-#ifndef VSIG_NO_PAIRLD
   constexpr int kQ = 3 * P::N / 4;
   if (hop == kQ && s0 >= 0 && s0 + kQ + P::N <= n) {      // uniform
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -129,7 +128,6 @@ __device__ __forceinline__ void load_pair_x4(float2* a, float2* d, const float2*
     for (int i = 2; i < P::E / 2; ++i) unpack(d, 2 * i, u[6 + i]);
     return;
   }
-#endif
   load_segment_x4<P>(a, x, s0, n, t);
   load_segment_x4<P>(d, x, s0 + hop, n, t);
 }

@@ -131,10 +131,6 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
       });
     }
   };
-#ifdef VSIG_PFB_FWD_ONLY        // tuning builds: every group walks forward
-  if (inside) walk(IC<0>{}, IC<0>{});
-  else walk(IC<0>{}, IC<1>{});
-#else
   if (gid & 1) {
     if (inside) walk(IC<1>{}, IC<0>{});
     else walk(IC<1>{}, IC<1>{});
@@ -142,14 +138,13 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
     if (inside) walk(IC<0>{}, IC<0>{});
     else walk(IC<0>{}, IC<1>{});
   }
-#endif
 }
 
 // Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3;
-// C = 64: registers capped for 4 waves / SIMD, VAR 7), 64 frames per group.
-#ifndef VSIG_PFB_VAR64
-#define VSIG_PFB_VAR64 7
-#endif
+// C = 64: registers capped for 4 waves / SIMD, VAR 7), 64 frames per group
+// (128 / 256 / 512 measured slower, profiles/r02_v13_pfb_ab.txt).
+constexpr int kPfbVar64 = 7;
+constexpr long long kPfbFramesPerGroup = 64;
 template <class PL, int PT>
 static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
                          const float2* tw, hipStream_t st) {
@@ -157,14 +152,11 @@ static void launch_pfb_t(const float2* x, long long n, const float* h, long long
   constexpr int step = E * (PT / cgcd(E, PT));
   // frames per group: a multiple of the unrolled step, so the (PT-1)-row ring
   // prologue stays a small fraction of the group's reads
-#ifndef VSIG_PFB_FPG
-#define VSIG_PFB_FPG 64
-#endif
-  constexpr long long want = VSIG_PFB_FPG;
+  constexpr long long want = kPfbFramesPerGroup;
   const long long fpg = ((want + step - 1) / step) * step;
   const long long groups = (M + fpg - 1) / fpg;
   const long long blocks = (groups + G - 1) / G;
-  hipLaunchKernelGGL((pfb_kernel<PL, PT, PL::N == 64 ? VSIG_PFB_VAR64 : 3>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M,
+  hipLaunchKernelGGL((pfb_kernel<PL, PT, PL::N == 64 ? kPfbVar64 : 3>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M,
                      fpg, y, tw);
 }
 

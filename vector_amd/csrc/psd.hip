@@ -275,7 +275,6 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                       long long hop, float scale, float* out, long long nframes, int shift,
                       const float2* tw, hipStream_t st) {
   if (nframes <= 0) return hipSuccess;
-#ifndef VSIG_NO_ILV
   if (N == 8192) {      // interleaved first / last pass: 16-byte loads, 8-byte stores
     const bool x4 = stride == 1 && nperseg == N && hop % 2 == 0 &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(win) & 7) == 0;
@@ -283,7 +282,6 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
                        0, st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, x4);
     return hipGetLastError();
   }
-#endif
   VSIG_PLAN_SWITCH(N, {
     if constexpr (PL::TF >= 256) {
       hipLaunchKernelGGL(psd_pair_kernel<PL>, dim3((unsigned)((nframes + 1) / 2)), dim3(PL::TF), 0,

@@ -204,7 +204,6 @@ hipError_t launch_c64_to_planar(const float2* x, long long n, float* re, float* 
 
 #ifdef VSIG_TUNING
 namespace vsig {
-int g_tune_fir_grid = 0, g_tune_xcorr_grid = 0;
 
 // ---------------------------------------------------------------- copy probe
 // HBM ceiling probe for the tuning tools (tools/membw.py): copy n complex64

@@ -222,13 +222,12 @@ int os_size_fir(int ntaps) {
   if (ntaps <= 8192) return 16384;
   return 0;
 }
-#ifndef VSIG_XCORR_BIG_FROM
-#define VSIG_XCORR_BIG_FROM 8193     // templates from this length use M = 32768
-#endif
+// templates of 8193 .. 16384 samples use M = 32768 (measured slower than
+// M = 16384 for shorter ones, xcorr.hip PlanX32k)
 int os_size_xcorr(long long L) {
   if (L <= 1024) return 4096;
   if (L <= 2048) return 8192;
-  if (L < VSIG_XCORR_BIG_FROM && L <= 8192) return 16384;
+  if (L <= 8192) return 16384;
   if (L <= 16384) return 32768;
   return 0;
 }
@@ -558,12 +557,6 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else if (k == "blas_threads") {
     if (value < 1 || value > 1024) return fail(c, VSIG_E_INVALID, "blas_threads must be in [1, 1024]");
     c->blas_threads = value;
-#ifdef VSIG_TUNING
-  } else if (k == "tune_fir_grid") {
-    vsig::g_tune_fir_grid = value > 0 ? value : 0;
-  } else if (k == "tune_xcorr_grid") {
-    vsig::g_tune_xcorr_grid = value > 0 ? value : 0;
-#endif
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }
@@ -747,13 +740,11 @@ int vsig_fir_create(vsig_ctx* c, const void* taps, int32_t ntaps, int32_t decim,
   if (!M) return fail(c, VSIG_E_UNSUPPORTED, "no block size for ntaps");
   long long hop = ((long long)M - (ntaps - 1)) / decim * decim;
   if (hop < 1) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
-#ifndef VSIG_FIR1_NO_HOP768
   // 1024-point pairs at hop 768 (ntaps 225..257): the second segment's first
   // quarter comes from the first one's registers (load_pair_x4), 14 loads per
   // pair instead of 16 for <= 4 % more segments (0.84 -> 0.80 ms at config 2,
   // profiles/r03_pl1_ab.txt)
   if (M == 1024 && decim == 1 && hop > 768 && hop < 800) hop = 768;
-#endif
   float2* hd = nullptr;
   HIPCHK(c, hipMalloc(&hd, (size_t)ntaps * sizeof(float2)));
   hipError_t e = hipMemcpyAsync(hd, taps, (size_t)ntaps * sizeof(float2), hipMemcpyHostToDevice, c->stream);
@@ -815,7 +806,6 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
     const int lo2 = (f->ntaps - 1 + D - 1) / D * D;
     const long long hop = (long long)(f->M - lo2) / D * D;
     if (hop < D) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
-#ifndef VSIG_FIR_DEC_FOLD
     if (f->G) {      // D = 4: polyphase form (fir_poly_kernel)
       if ((rc = get_twiddles(c, 256, &tw)) || (rc = get_twiddles(c, -256, &twd))) return rc;
       Timed t(c, "fir");
@@ -823,7 +813,6 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
                                       twd, c->stream, mix));
       return VSIG_OK;
     }
-#endif
     if ((rc = get_twiddles(c, -1024, &tw)) || (rc = get_twiddles(c, -1024 / f->decim, &twd))) return rc;
     Timed t(c, "fir");
     HIPCHK(c, vsig::launch_fir_dec(D, (const float2*)x, nhist + n, nhist, f->Hs, lo2, hop, (float2*)y,

@@ -130,9 +130,6 @@ int xcorr_lane_keys(int M);
 // items): ob + wstep w + l + 64 (q % rsub) + stride (q / rsub), l < 64, q < Q.
 hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* wstep, int* rsub);
 #ifdef VSIG_TUNING
-// Tuning: persistent grids for the D = 4 FIR and the M = 16384 correlator (0:
-// the normal launch), set by vsig_set_option "tune_fir_grid" / "tune_xcorr_grid".
-extern int g_tune_fir_grid, g_tune_xcorr_grid;
 // Tuning micro-benchmarks: iters FFTs per frame, frames blocks (key: plan key).
 hipError_t launch_fft_bench(int key, float2* io, int frames, int iters, const float2* tw, int twl,
                             hipStream_t st);

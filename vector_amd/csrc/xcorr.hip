@@ -20,8 +20,7 @@ namespace vsig {
 // sum of template chunks).
 // Partials: one per wave.  Wave w of block b covers the outputs
 //   b*hop + 64 w + l + TF q,   l < 64, q < Q   (Q = E, or 2 E for the half
-// kernel; the interleaved half kernel: b*hop + 128 w + [0, 128) + 512 q'),
-// which refine.hip uses to revisit a wave's outputs (xcorr_geom).
+// kernel), which refine.hip uses to revisit a wave's outputs (xcorr_geom).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ void put_c(float2* p, float2 v, bool accum) {
   *p = accum ? cadd(*p, v) : v;
@@ -116,89 +115,42 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
 // The two halves go through fft_pair (LDS stores of one half overlap the
 // other's butterflies), twiddles from register anchors.
 // With P palindromic, in_index == out_index, and W_M^j = W_M^base * W_64^K(e)
-// (half_root): per-thread twiddles from the table wt (one, or two for the
-// interleaved map whose thread holds j = 2t and 2t + 1) and a compile-time 64th
-// root per element.  The interleaved plan (Plan8192i, tuning builds) reads each
-// half with 16-byte loads when every segment start is 16-byte aligned (hop
-// even: the API rounds M - L + 1 down to even at M = 16384).
+// (half_root): one per-thread twiddle from the table wt and a compile-time
+// 64th root per element.
 // ---------------------------------------------------------------------------
 // The M = 32768 correlator (templates of 8193 .. 16384 samples in one pass):
 // 16384-point halves, 512 threads x 32 values, 3 passes, one block per CU.
-// Measured on templates of 4096 (VSIG_XCORR_BIG_FROM=2049 builds): 1.89 ms
-// per 2^28 samples against 1.42 ms for the M = 16384 kernel (r02_v6 A/B), so
-// shorter templates keep M = 16384.
+// Measured on templates of 4096 (round 2): 1.89 ms per 2^28 samples against
+// 1.42 ms for the M = 16384 kernel (r02_v6 A/B), so shorter templates keep
+// M = 16384.
 using PlanX32k = Plan16384w;
-// Default: the sigma map (conflict-free exchanges, 8-byte loads).  The
-// interleaved map (16-byte loads, two split twiddles per thread; tuning build
-// VSIG_XCORR_ILV) measured slower here: 2.67 vs 2.58 ms at config 5, 1.316 vs
-// 1.277 at config 2 (profiles/r02_v19_ab.txt).
-#if defined(VSIG_NO_SWZ)
-using PlanX16k = Plan8192;
-#elif defined(VSIG_XCORR_ILV)
-using PlanX16k = Plan8192i;
-#elif defined(VSIG_XCORR_W)
-using PlanX16k = Plan8192w;
-#else
+// The sigma map (conflict-free exchanges, 8-byte loads).  Measured against
+// it (round 2-3): the interleaved map (16-byte loads, two split twiddles per
+// thread) 2.67 vs 2.58 ms at config 5 (profiles/r02_v19_ab.txt); the
+// 512-thread, 16-value Plan8192w (4 waves per SIMD, a third exchange per half)
+// 2.67 vs 2.48 ms (r03_v11).
 using PlanX16k = Plan8192x;
-#endif
-// twiddle-table key of PlanX16k (plan_info: -8192 = Plan8192w)
-constexpr int kPlanX16kKey = std::is_same<PlanX16k, Plan8192w>::value ? -8192 : 8192;
 
-// in_index(t, e) = base(t, b) + off(e), b = e / R0: the split twiddle
-// W_M^in_index = W_M^base * W_64^half_root(e).  Plain / sigma maps: one base
-// per thread (b's TF step is in off); the interleaved map: base 2t + b (two
-// per-thread twiddles), off = (e % R0) N / R0.
-template <class P>
-constexpr bool plan_ilv() { return map0_of<P>::value == kMapIlv; }
+// in_index(t, e) = base(t) + off(e): the split twiddle
+// W_M^in_index = W_M^base * W_64^half_root(e).
 template <class P, int M>
 constexpr int half_root(int e) {
-  return plan_ilv<P>() ? ((e % P::R[0]) * (P::N / P::R[0])) / (M / 64)
-                       : ((e / P::R[0]) * P::TF + (e % P::R[0]) * (P::N / P::R[0])) / (M / 64);
+  return ((e / P::R[0]) * P::TF + (e % P::R[0]) * (P::N / P::R[0])) / (M / 64);
 }
 
 template <class P>
 __device__ __forceinline__ void load_halves(float2* a, float2* d, const float2* __restrict__ x,
-                                            long long s0, long long n, int t, bool x4) {
+                                            long long s0, long long n, int t) {
   constexpr int H = P::N;
   const float2* base = x + s0;
-  if constexpr (plan_ilv<P>()) {
-    // interleaved operands x[2t + b + (N/R0) r]: one 16-byte load per r and half
-    // (x + s0 16-byte aligned: the launch's x4)
-    constexpr int R0 = P::R[0], S0 = P::N / R0;
-    static_assert(P::E == 2 * R0, "two butterflies per thread");
-    if (x4 && s0 >= 0 && s0 + 2 * H <= n) {
-      typedef float f4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-      for (int r = 0; r < R0; ++r) {
-        const f4 p = *reinterpret_cast<const f4*>(base + 2 * t + S0 * r);
-        const f4 q = *reinterpret_cast<const f4*>(base + H + 2 * t + S0 * r);
-        a[r] = make_float2(p.x, p.y);
-        a[R0 + r] = make_float2(p.z, p.w);
-        d[r] = make_float2(q.x, q.y);
-        d[R0 + r] = make_float2(q.z, q.w);
-      }
-      return;
-    }
-  }
-  if (s0 >= 0 && s0 + 2 * H <= n) {
-#ifndef VSIG_NO_BUFLD
-    if constexpr (!plan_ilv<P>()) {   // one voffset per thread, the rest in soffset
-      const auto rs = make_rsrc(base, 2u * H * (unsigned)sizeof(float2));
-      const unsigned v0 = (unsigned)in_index<P>(t, 0) * (unsigned)sizeof(float2);
-      static_for<0, P::E>([&](auto ei) {
-        constexpr int e = decltype(ei)::value;
-        a[e] = buf_load2(rs, v0, in_off<P>(e) * (int)sizeof(float2));
-        d[e] = buf_load2(rs, v0, (in_off<P>(e) + H) * (int)sizeof(float2));
-      });
-      return;
-    }
-#endif
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const unsigned i = (unsigned)in_index<P>(t, e);
-      a[e] = base[i];
-      d[e] = base[i + H];
-    }
+  if (s0 >= 0 && s0 + 2 * H <= n) {     // one voffset per thread, the rest in soffset
+    const auto rs = make_rsrc(base, 2u * H * (unsigned)sizeof(float2));
+    const unsigned v0 = (unsigned)in_index<P>(t, 0) * (unsigned)sizeof(float2);
+    static_for<0, P::E>([&](auto ei) {
+      constexpr int e = decltype(ei)::value;
+      a[e] = buf_load2(rs, v0, in_off<P>(e) * (int)sizeof(float2));
+      d[e] = buf_load2(rs, v0, (in_off<P>(e) + H) * (int)sizeof(float2));
+    });
   } else {
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
@@ -229,11 +181,7 @@ struct KeyedRank {
       if (c(e) != kStep * rank(e)) return false;
     return true;
   }
-#ifdef VSIG_NO_KEYED     // tuning builds: the compare-and-select epilogue
-  static constexpr bool ok = false;
-#else
   static constexpr bool ok = check();
-#endif
 };
 
 // Epilogue of a half-frame block: a holds outputs i = out_index(t, e), d holds
@@ -272,15 +220,6 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     }
   }
   if (!partials) return;
-#ifdef VSIG_KO_XEPI       // tuning knock-out (results wrong): one sum per thread
-  {
-    float2 z = make_float2(0.f, 0.f);
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) z = cadd(z, cadd(a[e], d[e]));
-    wave_partial_f(z.x, 0, z.y, 0.f, rev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
-    return;
-  }
-#endif
   if constexpr (KeyedRank<P>::ok) {
     // Per-thread argmax by key: the bits of |c|^2 (>= 0, so they order as the
     // floats) with the low 6 mantissa bits replaced by the output's rank in
@@ -311,14 +250,8 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
       } else {
         key = k > key ? k : key;
         any = true;
-#if defined(VSIG_KO_XSQRT)  // tuning knock-out: the sum of |c| without the square roots
-        s1 += a2 * 0.5f;
-        s2 += a2;
-#elif defined(VSIG_KO_SUMS) // tuning knock-out: no sums at all
-#else
         s1 += __builtin_amdgcn_sqrtf(a2);
         s2 += a2;
-#endif
       }
     };
     if (DV >= 0 && lim == hop) {       // interior block, compile-time split
@@ -348,11 +281,7 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     static_for<0, P::E>([&](auto ei) {
       constexpr int e = decltype(ei)::value;
       constexpr int c0 = KR::kStep * KR::rank(e);
-#ifdef VSIG_NO_DSKIP      // tuning builds: every element masked per lane
-      if constexpr (false) {
-#else
       if constexpr (KR::kStep == P::TF) {      // m(t) < TF = kStep
-#endif
         if (c0 + KR::kStep <= cut) acc(d[e], 0, KR::rank(e) + P::E, IC<0>{});
         else if (c0 < cut) acc(d[e], out_index<P>(t, e) + H, KR::rank(e) + P::E, IC<1>{});
       } else {
@@ -361,19 +290,10 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
     });
     }
     // lane keys (refine candidates per thread column, see xcorr_lane_keys)
-#ifndef VSIG_KO_LKEY      // tuning knock-out (refine inputs wrong): no lane-key store
     if (lkeys) lkeys[b * P::TF + tmapl<P>(t)] = key;
-#endif
     const int rank = (int)((key & 63u) ^ rx);
     const int mi = tmapl<P>(t) + KR::kStep * rank;
     const float m = any ? __uint_as_float(key & ~63u) : -1.f;
-#ifdef VSIG_KO_PART       // tuning knock-out: one lane stores the thread's values, no wave reduction
-    if ((t & 63) == 0) {
-      PeakPartial r{(double)m, (long long)mi, (double)s1, (double)s2};
-      partials[b * (P::TF / 64) + (t >> 6)] = r;
-    }
-    return;
-#endif
     wave_partial_f(m, mi, s1, s2, kRev, ob, nout, partials + b * (P::TF / 64) + (t >> 6));
     };
     if (rev) keyed(IC<1>{});
@@ -417,131 +337,87 @@ __device__ __forceinline__ void xcorr_half_epilogue(const float2* a, const float
 template <class P>
 constexpr int xcorr_waves_per_eu() { return P::E <= 16 ? 4 : P::TF >= 512 ? 1 : 2; }
 
-template <class P, bool PERSIST = false, int DV = -1>
+// The segment prefetch distance: one 4-byte load per 128-byte line of the
+// segment kSegPfDist blocks ahead -- about the block that takes this slot of
+// the XCD next (xcd_remap hands each XCD a contiguous run, two blocks per CU x
+// 32 CUs in flight) -- so that its loads find the lines in L2 instead of HBM.
+// Issued just before the epilogue and consumed only at the end of the block,
+// so nothing waits for it.  Earlier issue loses: right after the segment loads
+// the 63-deep vmcnt makes the split step wait for the prefetch too (+14 %);
+// after the spectrum product the lines live long enough in the 4 MB L2 to be
+// evicted again (+45 % L2 fills).  Distances 32 / 96 / 128 / 192 / 256 are
+// slower or equal.  profiles/r03_v22_xcorr_segpf_ab.txt: -5 % correlator
+// time, +2.5 % reads.
+constexpr int kSegPfDist = 64;
+
+template <class P, int DV = -1>
 __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_kernel(
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw,
-    const float2* __restrict__ wt, bool x4, unsigned* __restrict__ lkeys) {
+    const float2* __restrict__ wt, unsigned* __restrict__ lkeys) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
+  static_assert(map0_of<P>::value != kMapIlv, "one split twiddle per thread");
   constexpr int M = 2 * P::N;
   static_assert(P::TF % (M / 64) == 0 && (P::N / P::R[0]) % (M / 64) == 0,
                 "per-element split twiddles must be 64th roots of unity");
   __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
-  const int t0 = threadIdx.x;
+  const int t = threadIdx.x;
   float2 wa[nanch_total<P>()];
-  load_anchors<P>(wa, tw, t0);
-  // PERSIST (tuning builds): a fixed grid walks the blocks (grid-stride)
-  for (long long it = PERSIST ? blockIdx.x : 0;; it += gridDim.x) {
-  const long long b = PERSIST ? it : xcd_remap(blockIdx.x, gridDim.x);
+  load_anchors<P>(wa, tw, t);
+  const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (b >= nblocks) return;
-  if constexpr (PERSIST) __syncthreads();        // the previous block's LDS reads
-  // per-iteration thread index and tables opaque to LICM (else every
-  // iteration's addresses and table loads are hoisted and pinned in VGPRs)
-  const int zz = PERSIST ? opaque_zero() : 0;
-  const int t = t0 + zz;
-  const float4* __restrict__ Psz = Ps2 + zz;
-  const float2* __restrict__ wtz = wt + zz;
   auto fft2 = [&](float2* x, float2* y) {
     launder_anchors<P>(wa);
     fft_pair<P>(x, y, lds, TwAnchors{wa}, t);
   };
-  // W_M^base: base = in_index(t, 0) (and in_index(t, R0) for the interleaved
-  // map), loaded ahead of the segment and the prefetch below (loads complete in
-  // issue order)
-  const float2 w = wtz[in_index<P>(t, 0)];
-  const float2 w1 = plan_ilv<P>() ? wtz[in_index<P>(t, P::R[0])] : w;
+  // W_M^base: base = in_index(t, 0), loaded ahead of the segment and the
+  // prefetch below (loads complete in issue order)
+  const float2 w = wt[in_index<P>(t, 0)];
   float2 a[P::E], d[P::E];
-#ifdef VSIG_KO_SEGLD      // tuning knock-out (results wrong): no segment loads
-  static_for<0, P::E>([&](auto ei) {
-    constexpr int e = decltype(ei)::value;
-    a[e] = make_float2((float)(t + e), (float)b);
-    d[e] = make_float2((float)(t - e), 1.f);
-  });
-#else
-  load_halves<P>(a, d, s, b * hop - off, n, t, x4);
-#endif
-  // Segment prefetch: one 4-byte load per 128-byte line of the segment
-  // VSIG_SEGPF_DIST blocks ahead -- about the block that takes this slot of the
-  // XCD next (xcd_remap hands each XCD a contiguous run, two blocks per CU x 32
-  // CUs in flight) -- so that its loads find the lines in L2 instead of HBM.
-  // Issued just before the epilogue (VSIG_SEGPF_POS 2) and consumed only at
-  // the end of the block, so nothing waits for it.  Earlier issue loses: right
-  // after the segment loads (0) the 63-deep vmcnt makes the split step wait
-  // for the prefetch too (+14 %); after the spectrum product (1) the lines
-  // live long enough in the 4 MB L2 to be evicted again (+45 % L2 fills).
-  // profiles/r03_v22_xcorr_segpf_ab.txt: -5 % correlator time, +2.5 % reads.
+  load_halves<P>(a, d, s, b * hop - off, n, t);
   constexpr int kPfLines = 2 * P::N * 8 / 128 / P::TF;          // 128-byte lines per thread
   float pfv[kPfLines];
 #pragma unroll
   for (int k = 0; k < kPfLines; ++k) pfv[k] = 0.f;
-#ifndef VSIG_SEGPF_DIST
-#define VSIG_SEGPF_DIST 64
-#endif
-#ifndef VSIG_SEGPF_POS
-#define VSIG_SEGPF_POS 2
-#endif
-  auto prefetch = [&]() {
-#ifndef VSIG_NO_SEGPF
-    if constexpr (!PERSIST) {
-      const long long bn = b + VSIG_SEGPF_DIST;
-      const long long s0 = bn * hop - off;
-      if (bn < nblocks && s0 >= 0 && s0 + 2 * P::N <= n) {
-        const float* q = reinterpret_cast<const float*>(s + s0);
-#pragma unroll
-        for (int k = 0; k < kPfLines; ++k) pfv[k] = q[(t + k * P::TF) * 32];
-      }
-    }
-#endif
-  };
-  if constexpr (VSIG_SEGPF_POS == 0) prefetch();
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
     const float2 x0 = a[e], x1 = d[e];
     a[e] = cadd(x0, x1);
-    d[e] = twc<half_root<P, M>(e), 64>(cmul(csub(x0, x1), (plan_ilv<P>() && e >= P::R[0]) ? w1 : w));
+    d[e] = twc<half_root<P, M>(e), 64>(cmul(csub(x0, x1), w));
   });
   fft2(a, d);
-#ifndef VSIG_NO_BUFLD
-  if constexpr (!plan_ilv<P>()) {
-    const auto rp = make_rsrc(Psz, (unsigned)P::N * (unsigned)sizeof(float4));
+  {
+    const auto rp = make_rsrc(Ps2, (unsigned)P::N * (unsigned)sizeof(float4));
     const unsigned v0 = (unsigned)out_index<P>(t, 0) * (unsigned)sizeof(float4);
     static_for<0, P::E>([&](auto ei) {
       constexpr int e = decltype(ei)::value;
-#ifdef VSIG_KO_TMPLD      // tuning knock-out (results wrong): no template-spectrum loads
-      const float4 p = make_float4(0.5f, 0.25f, (float)e, 0.125f);
-#else
       const float4 p = buf_load4(rp, v0, out_off<P>(e) * (int)sizeof(float4));
-#endif
       a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
       d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
     });
-  } else
-#endif
-  {
-#pragma unroll
-    for (int e = 0; e < P::E; ++e) {
-      const float4 p = Psz[out_index<P>(t, e)];
-      a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
-      d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
-    }
   }
-  if constexpr (VSIG_SEGPF_POS == 1) prefetch();
   fft2(a, d);
   static_for<0, P::E>([&](auto ei) {
     constexpr int e = decltype(ei)::value;
-    const float2 o = twc<half_root<P, M>(e), 64>(cmul(d[e], (plan_ilv<P>() && e >= P::R[0]) ? w1 : w));
+    const float2 o = twc<half_root<P, M>(e), 64>(cmul(d[e], w));
     const float2 ev = a[e];
     a[e] = cadd(ev, o);
     d[e] = csub(ev, o);
   });
-  if constexpr (VSIG_SEGPF_POS == 2) prefetch();
+  {                                          // the segment prefetch (kSegPfDist)
+    const long long bn = b + kSegPfDist;
+    const long long s0 = bn * hop - off;
+    if (bn < nblocks && s0 >= 0 && s0 + 2 * P::N <= n) {
+      const float* q = reinterpret_cast<const float*>(s + s0);
+#pragma unroll
+      for (int k = 0; k < kPfLines; ++k) pfv[k] = q[(t + k * P::TF) * 32];
+    }
+  }
   xcorr_half_epilogue<P, DV>(a, d, b, hop, nout, c, store_mode, partials, lkeys, t);
 #pragma unroll
   for (int k = 0; k < kPfLines; ++k)   // the prefetch loads stay; their values are never used
     asm volatile("" ::"v"(pfv[k]));
-  if constexpr (!PERSIST) return;
-  }
 }
 
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
@@ -552,41 +428,27 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
   if (lkeys && !xcorr_lane_keys(M)) return hipErrorInvalidValue;
   const long long nblocks = (nout + hop - 1) / hop;
   if (M == 16384) {
-    // every segment start s - off + b hop 16-byte aligned: 16-byte loads
-    const bool x4 = hop % 2 == 0 && ((reinterpret_cast<uintptr_t>(s) - 8 * (uintptr_t)off) & 15) == 0;
-#ifdef VSIG_TUNING
-    if (g_tune_xcorr_grid > 0) {
-      hipLaunchKernelGGL((xcorr_half_kernel<PlanX16k, true>), dim3((unsigned)g_tune_xcorr_grid),
-                         dim3(PlanX16k::TF), 0, st, s, n, reinterpret_cast<const float4*>(Ps), off, nout,
-                         hop, c, store_mode, partials, nblocks, tw, wt, x4, lkeys);
-      return hipGetLastError();
-    }
-#endif
     // interior blocks keep the second half's ranks below (hop - H) / kStep: the
     // common split (hop = 12288: L = 4096, 4097) has its compile-time epilogue
     using KR = KeyedRank<PlanX16k>;
     constexpr int kDv = PlanX16k::E / 2;
     const long long cut = hop - PlanX16k::N;
     const bool dv = KR::ok && KR::kStep == PlanX16k::TF && cut == (long long)kDv * KR::kStep;
-#ifdef VSIG_NO_DVSPLIT    // tuning builds: the runtime split for every block
-    if (false) {
-#else
     if (dv) {
-#endif
-      hipLaunchKernelGGL((xcorr_half_kernel<PlanX16k, false, kDv>), dim3((unsigned)nblocks),
+      hipLaunchKernelGGL((xcorr_half_kernel<PlanX16k, kDv>), dim3((unsigned)nblocks),
                          dim3(PlanX16k::TF), 0, st, s, n, reinterpret_cast<const float4*>(Ps), off, nout,
-                         hop, c, store_mode, partials, nblocks, tw, wt, x4, lkeys);
+                         hop, c, store_mode, partials, nblocks, tw, wt, lkeys);
       return hipGetLastError();
     }
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt, x4, lkeys);
+                       partials, nblocks, tw, wt, lkeys);
     return hipGetLastError();
   }
   if (M == 32768) {     // 16384-point halves, one block per CU
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX32k>, dim3((unsigned)nblocks), dim3(PlanX32k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt, false, lkeys);
+                       partials, nblocks, tw, wt, lkeys);
     return hipGetLastError();
   }
   auto run = [&](auto plan) {
@@ -624,15 +486,8 @@ hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* ws
   *wstep = 64;
   *rsub = 1;
   if (M == 32768) { *waves = PlanX32k::TF / 64; *Q = 2 * PlanX32k::E; *stride = PlanX32k::TF; *plan = -16384; }
-  else if (M == 16384 && plan_ilv<PlanX16k>()) {
-    // thread t holds j = 2t + b + (N/R0) r (+ N for the second half): wave w's
-    // outputs are 128 w + [0, 128) + (N/R0) r + N h -- two 64-output rows per
-    // step of N/R0 (= 512), 2 E rows in all
-    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::N / PlanX16k::R[0];
-    *wstep = 128; *rsub = 2; *plan = 8192;
-  }
   else if (M == 16384) {
-    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::TF; *plan = kPlanX16kKey;
+    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::TF; *plan = 8192;
   }
   else if (M == 8192) { *waves = Plan8192::TF / 64; *Q = Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 4096) { *waves = Plan4096::TF / 64; *Q = Plan4096::E; *stride = Plan4096::TF; *plan = 4096; }
