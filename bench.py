@@ -97,6 +97,38 @@ def cpu_baseline(samples, taps, nfft, tmpl, decim=1):
                 seconds=round(dt, 3))
 
 
+def cpu_allowance():
+    """(cores this process may use, how that was determined): the affinity
+    mask, capped by a cgroup CPU quota (v2 cpu.max, v1 cfs_quota_us) where one
+    is set; OMP_NUM_THREADS (the pool sets it to the box's CPU share) is
+    recorded and caps it too."""
+    aff = len(os.sched_getaffinity(0))
+    n, src = aff, [f"sched_getaffinity={aff}"]
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = int(q) / int(per)
+    except (OSError, ValueError):
+        try:
+            q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+            per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+            if q > 0:
+                quota = q / per
+        except (OSError, ValueError):
+            pass
+    if quota is not None:
+        src.append(f"cgroup quota {quota:g} cores")
+        n = min(n, max(1, int(quota)))
+    else:
+        src.append("no cgroup quota")
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        src.append(f"OMP_NUM_THREADS={omp}")
+        n = min(n, int(omp))
+    return n, ", ".join(src)
+
+
 def cpu_baseline_allcores(samples, taps, nfft, tmpl, workers, decim=1):
     """The same CPU chain as cpu_baseline on `workers` processes, one time
     chunk each with its halos (SURVEY.md §8(d)'s all-cores variant); value =
@@ -168,40 +200,58 @@ WORKLOADS = {
 }
 
 
-def _free_port() -> int:
-    import socket
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so:
-        so.bind(("127.0.0.1", 0))
-        return so.getsockname()[1]
-
-
 def launch_ranks(n: int, argv: list[str]) -> int:
     """`bench.py --gpus N` without a launcher: start N child processes of this
     script (one per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
     127.0.0.1) -- before anything here touches the GPU, and as children, never
-    by exec.  Rank 0's stdout carries the one JSON line.  Returns the first
-    non-zero child exit code (the others are stopped then), else 0."""
+    by exec.  The parent holds the rendezvous store itself (bound to a free port
+    before any child starts, as torchrun's agent does: the children connect as
+    clients, so no port can be taken in between).  Rank 0's stdout carries the
+    one JSON line.  Returns the first non-zero child exit code (the others are
+    stopped then), else 0; on SIGTERM / Ctrl-C the children are stopped too."""
+    import signal
     import subprocess
-    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    from torch.distributed import TCPStore
+    store = TCPStore("127.0.0.1", 0, world_size=None, is_master=True, wait_for_workers=False)
+    port = str(store.port)
     procs = []
-    for r in range(n):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
-                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv], env=env))
+
+    def _term(signum, frame):
+        raise SystemExit(128 + signum)
+    old = signal.signal(signal.SIGTERM, _term)
     rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                log(f"bench: rank {procs.index(p)} exited with {code}; stopping the others")
-                for q in live:
-                    q.terminate()
-        time.sleep(0.05)
+    try:
+        for r in range(n):
+            env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                       LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
+                       TORCHELASTIC_USE_AGENT_STORE="True", TORCHELASTIC_RESTART_COUNT="0")
+            procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
+                                          env=env))
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 1
+                    log(f"bench: rank {procs.index(p)} exited with {code}; stopping the others")
+                    for q in live:
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        signal.signal(signal.SIGTERM, old)
+        for p in procs:                   # nothing outlives the launcher
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=15)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        del store
     return rc
 
 
@@ -380,8 +430,9 @@ def main():
                     help="CPU-baseline sample (default: ~10-15 s of single-core work: "
                          "2**26 samples for the chains, 2**24 for sync, 2**27 for pfb)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-workers", type=int, default=16,
-                    help="processes for the all-cores CPU baseline (the GPU box's CPU share is 16)")
+    ap.add_argument("--cpu-workers", type=int, default=None,
+                    help="processes for the all-cores CPU baseline (default: this process's CPU "
+                         "allowance, bench.cpu_allowance, within host memory)")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-refine", action="store_true",
                     help="skip the correlator's exact-argmax refine pass (A/B only)")
@@ -448,11 +499,26 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         cs = args.cpu_samples or (1 << 26)
         cpu = cpu_baseline(cs, taps, args.nfft, tmpl, decim)
-        cpu["cores_available"] = len(os.sched_getaffinity(0))
-        if args.cpu_workers > 1:
+        ncores, src = cpu_allowance()
+        cpu["cores_available"] = ncores
+        cpu["cores_source"] = src
+        workers = args.cpu_workers or ncores
+        # ~2 GB of numpy arrays per worker (a 2**25-sample chunk through
+        # np.convolve / spectrogram / np.correlate complex128): stay within
+        # half of the host memory available now
+        try:
+            import psutil
+            cap = max(1, int(psutil.virtual_memory().available * 0.5 // (2 << 30)))
+            if workers > cap:
+                src += f"; {workers} -> {cap} workers for host memory"
+                workers = cap
+        except ImportError:
+            pass
+        if workers > 1:
             try:
-                cpu["all_cores"] = cpu_baseline_allcores(cs // 2, taps, args.nfft, tmpl,
-                                                         args.cpu_workers, decim)
+                cpu["all_cores"] = cpu_baseline_allcores(cs // 2, taps, args.nfft, tmpl, workers,
+                                                         decim)
+                cpu["all_cores"]["cores_source"] = src
             except Exception as e:       # the GPU number stands without it
                 cpu["all_cores"] = {"error": repr(e)[:200]}
     out = {
@@ -554,7 +620,8 @@ def run_sync(args, world, rank, local, dev):
                    sample=(f"{ns} samples (2**{int(np.log2(ns))}) through np.correlate complex128 L={L} valid + "
                            f"find_correlation_peak, {dt:.2f} s, 1 thread (direct O(N L); the "
                            f"full 2**30 stream would take ~{n / (ns / dt) / 60:.0f} min)"),
-                   seconds=round(dt, 3), cores_available=len(os.sched_getaffinity(0)))
+                   seconds=round(dt, 3), cores_available=cpu_allowance()[0],
+                   cores_source=cpu_allowance()[1])
     out = {
         "metric": "Msamples/s c64 through the sliding-correlation sync (BASELINE config 3)",
         "value": round(n / (elapsed / args.steps) / 1e6, 1), "unit": "Msamples/s",

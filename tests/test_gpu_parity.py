@@ -191,6 +191,24 @@ def test_filter_long_taps_vs_oracle(gpu, ntaps, n, decim):
     assert_normwise(gpu.filter(x, taps, decim), ref.fir_filter(x, taps, decim), FIR_TOL)
 
 
+@pytest.mark.parametrize("ntaps,nhist,decim", [(9000, 8999, 1), (9000, 3000, 4), (20_000, 19_999, 4),
+                                               (20_000, 12_345, 1)])
+def test_filter_long_taps_with_history(gpu, ntaps, nhist, decim):
+    """The time-chunk form (FirFilter(x, nhist=...), what StreamChain and the
+    native chain call per rank) for filters over 8192 taps: the parts' outputs
+    are delayed into place past the history.  Against np.convolve over
+    [history | chunk] (samples before the history are zeros)."""
+    import torch
+    rng = np.random.default_rng(ntaps + nhist)
+    n = 30_000
+    xe = ref.synth_iq(nhist + n, seed=nhist)
+    taps = (rng.standard_normal(ntaps) / np.sqrt(ntaps)).astype(np.float32)
+    f = gpu.FirFilter(taps, decim)
+    y = f(torch.from_numpy(xe).cuda(), nhist=nhist).cpu().numpy()
+    want = np.convolve(xe, taps)[nhist: nhist + n][::decim]
+    assert_normwise(y, want, FIR_TOL)
+
+
 def test_filter_real_input_real_output(gpu):
     rng = np.random.default_rng(6)
     x = rng.standard_normal(10_000)

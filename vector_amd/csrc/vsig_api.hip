@@ -794,6 +794,7 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
       return rc;
     for (size_t j = 0; j < f->parts.size(); ++j) {
       if ((rc = fir_exec(f->parts[j], x, 0, nz, f->z, nz, nullptr))) return rc;
+      Timed t(c, "fir");
       HIPCHK(c, vsig::launch_fir_part_accum(f->z, nz, nhist - (long long)j * kFirPartTaps, f->decim, ny,
                                             j == 0, (float2*)y, c->stream));
     }
