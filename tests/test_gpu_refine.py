@@ -263,6 +263,47 @@ def test_flat_valid_confidence_exact(gpu):
     assert gpu.find_correlation_peak(c, lags) == (want_lag, want_val, want_conf)
 
 
+@pytest.mark.parametrize("na,nv,mode,dt", [
+    (20_000, 1000, "full", np.complex128),     # a slides (the template is the shorter operand)
+    (1000, 20_000, "full", np.complex128),     # v slides (np.correlate's swapped order)
+    (1000, 20_000, "valid", np.complex64),
+    (30_000, 3000, "same", np.complex64),
+    (40_000, 12_000, "valid", np.complex128),  # > 10000 terms: OpenBLAS's thread split
+    (12_000, 40_000, "full", np.complex64)])
+def test_flat_dense_every_geometry(gpu, na, nv, mode, dt):
+    """The dense numpy-order form on a flat |c| (every full-overlap output in
+    the band) in both operand orders, every mode, both precisions and sums
+    over 10000 terms: the argmax, |c| and complex128 value equal numpy's bit
+    for bit (np.correlate complex128 = the reference's arithmetic), the
+    confidence to 1e-4."""
+    t = np.arange(max(na, nv))
+    tone = np.exp(2j * np.pi * 0.0123 * t).astype(dt)
+    a, v = tone[:na], tone[:nv]
+    # cross_correlate_signals(signal1=v, signal2=a) = np.correlate(a, v) in complex128
+    r = np.correlate(a.astype(np.complex128), v.astype(np.complex128), mode)
+    ar = np.abs(r)
+    c, lags = gpu.cross_correlate_signals(v, a, mode)
+    assert _status(gpu)[0] == 0
+    k = int(np.argmax(np.abs(c)))
+    assert k == int(np.argmax(ar))
+    assert np.abs(c)[k] == ar.max() and c[k] == r[k]
+    try:
+        want = ref.find_correlation_peak(r, lags)
+    except IndexError:                 # the reference's lag-axis quirks ('same' / long signal1)
+        with pytest.raises(IndexError):
+            gpu.correlate_peak(v, a, mode)
+        return
+    got = gpu.correlate_peak(v, a, mode)
+    assert got[0] == want[0]
+    assert got[1] == want[1]
+    # the confidence from the fused fp32 sums (the ramps of 'full' / 'same' give
+    # a wide spread) or, for a flat |c|, numpy's own statistics
+    assert got[2] == pytest.approx(want[2], rel=1e-4, abs=1e-7)
+    lag2, val2, conf2 = gpu.find_correlation_peak(c, lags)
+    assert (lag2, val2) == want[:2]
+    assert conf2 == pytest.approx(want[2], rel=1e-4, abs=1e-7)
+
+
 @pytest.mark.parametrize("n", [1, 7, 100, 8192, 8193, 50_000, (1 << 20) + 3])
 def test_abs_stats_numpy_order(gpu, n):
     """vsig_abs_stats_dev = np.mean(np.abs(a)), np.std(np.abs(a)) bit for bit
