@@ -96,7 +96,10 @@ static_assert(sizeof(RefineKeys) == 64, "the items follow the keys at +64 B");
 struct RefineSlot { double m; long long i; };   // one per numpy-pass block
 
 constexpr int kNpThreads = 256;
-constexpr int kNpGrid = 512;                   // 2 blocks per CU (64 KB of LDS each)
+#ifndef VSIG_NP_GRID
+#define VSIG_NP_GRID 512  // A/B: numpy-pass blocks
+#endif
+constexpr int kNpGrid = VSIG_NP_GRID;          // 2 blocks per CU (64 KB of LDS each)
 constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
 constexpr long long kBlasThreadMin = 10000;    // zdotu_k: threads only above this n
 constexpr long long kSparseMax = 4096;         // candidate outputs of the sparse form
