@@ -261,7 +261,10 @@ def _launcher_selftest(args, world, rank, local):
     dist.init_process_group("gloo")
     info = {k: os.environ.get(k) for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR",
                                            "MASTER_PORT")}
+    info["pid"] = os.getpid()
     json.dump(info, open(os.path.join(args.launcher_selftest, f"rank{rank}.json"), "w"))
+    if os.environ.get("VSIG_SELFTEST_HANG"):     # the launcher's cleanup test: stay alive
+        time.sleep(120)
     t = torch.tensor([rank + 1.0])
     dist.all_reduce(t)
     if rank == 0:

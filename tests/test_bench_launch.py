@@ -38,3 +38,37 @@ def test_self_launch_failure_propagates(tmp_path):
     non-zero instead of hanging on the collective."""
     r = _run(2, tmp_path / "missing" / "dir")
     assert r.returncode != 0
+
+
+def test_launcher_stops_children_on_sigterm(tmp_path):
+    """SIGTERM to the launcher stops its rank processes too (nothing that may
+    hold a GPU outlives it)."""
+    import signal
+    import time
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")}
+    env["VSIG_SELFTEST_HANG"] = "1"
+    p = subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2",
+                          "--launcher-selftest", str(tmp_path)], env=env,
+                         stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        deadline = time.time() + 120
+        while time.time() < deadline and not all((tmp_path / f"rank{k}.json").exists()
+                                                  for k in range(2)):
+            time.sleep(0.2)
+        time.sleep(0.5)
+        pids = [json.load(open(tmp_path / f"rank{k}.json"))["pid"] for k in range(2)]
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) != 0
+        for pid in pids:
+            for _ in range(100):
+                try:
+                    os.kill(pid, 0)
+                except ProcessLookupError:
+                    break
+                time.sleep(0.1)
+            else:
+                raise AssertionError(f"rank process {pid} still alive")
+    finally:
+        if p.poll() is None:
+            p.kill()

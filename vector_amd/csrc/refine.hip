@@ -240,6 +240,23 @@ __device__ __forceinline__ PeakPartial ld_agent(const PeakPartial* p) {
   return r;
 }
 
+// Cross-block hand-offs (a block's record, then its count on a counter): by
+// default an agent-scope fence per block (buffer_wbl2 + buffer_inv on
+// gfx950); VSIG_REFINE_RELAXED (A/B): the records as agent-scope atomic stores
+// completed (s_waitcnt) before the counter's atomic and read back with
+// agent-scope atomic loads -- no L2 write-back.
+#ifndef VSIG_REFINE_RELAXED
+#define VSIG_REFINE_RELAXED 0
+#endif
+constexpr bool kRelaxed = VSIG_REFINE_RELAXED != 0;
+
+__device__ __forceinline__ void st_agent(PeakPartial* o, const PeakPartial& r) {
+  __hip_atomic_store(&o->max2, r.max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->idx, r.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->sum_abs, r.sum_abs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->sum_abs2, r.sum_abs2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) {
   const int tid = threadIdx.x;
   __shared__ int slast, ncl;
@@ -259,12 +276,24 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
       s1 += p.sum_abs;
       s2 += p.sum_abs2;
     }
-    block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
+    if constexpr (kRelaxed) {
+      __shared__ PeakPartial r0[1];
+      block_partial<256>(m, mi, s1, s2, r0);
+      __syncthreads();
+      if (tid == 0) st_agent(f.tmp + blockIdx.x, r0[0]);
+    } else {
+      block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
+    }
   }
   if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
-    __threadfence();
-    slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
-    if (slast) __threadfence();
+    if constexpr (kRelaxed) {
+      __builtin_amdgcn_s_waitcnt(0);
+      slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
+    } else {
+      __threadfence();
+      slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
+      if (slast) __threadfence();
+    }
   }
   __syncthreads();
   if (!slast) return;
@@ -696,10 +725,17 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
   __syncthreads();
   if (tid == 0) {
     for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
-    slots[blockIdx.x] = RefineSlot{bm, bi};
-    __threadfence();
-    slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
-    if (slast) __threadfence();
+    if constexpr (kRelaxed) {
+      __hip_atomic_store(&slots[blockIdx.x].m, bm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&slots[blockIdx.x].i, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __builtin_amdgcn_s_waitcnt(0);
+      slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
+    } else {
+      slots[blockIdx.x] = RefineSlot{bm, bi};
+      __threadfence();
+      slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
+      if (slast) __threadfence();
+    }
   }
   __syncthreads();
   if (!slast) return;
