@@ -9,10 +9,7 @@ from vector_amd import _build  # noqa: E402
 # while its measurement is open; measured alternatives are deleted with it and
 # recorded in DESIGN.md, see round 3's list)
 VARIANTS = {
-    "libvsig_ntmid": ("VSIG_FIR_NTMID=1",),
-    "libvsig_relaxed": ("VSIG_REFINE_RELAXED=1",),
-    "libvsig_np256": ("VSIG_NP_GRID=256",),
-    "libvsig_np64": ("VSIG_NP_GRID=64",),
+    "libvsig_rtrace": ("VSIG_REFINE_TRACE=1",),
 }
 for name in (sys.argv[1:] or VARIANTS):
     _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)

@@ -1,0 +1,6 @@
+# round 4: refine phase timestamps (VSIG_REFINE_TRACE build) in the micro and the c5 bench
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+export VSIG_LIB=$GRAFT_REPO_ROOT/vector_amd/libvsig_rtrace.so
+timeout -k 10 120 python3 tools/refine_micro.py 6 > gpurun_out/r04_rtrace_micro.txt 2>&1
+timeout -k 10 300 python3 bench.py --steps 4 --warmup 1 --no-cpu-baseline --no-c2-leg > gpurun_out/r04_rtrace_c5.txt 2>&1

@@ -9,10 +9,6 @@
 
 namespace vsig {
 
-#ifndef VSIG_FIR_NTMID
-#define VSIG_FIR_NTMID 0
-#endif
-
 // Streaming accesses (input read once, output written once) with a
 // non-temporal hint where it measured faster on the chain: the PSD's frame
 // loads and the FIR's output stores (so the filtered stream does not sit in
@@ -115,16 +111,8 @@ __device__ __forceinline__ void load_pair_x4(float2* a, float2* d, const float2*
     typedef float f4 __attribute__((ext_vector_type(4)));
     const f4* b4 = reinterpret_cast<const f4*>(x + s0);
     f4 u[P::E / 2 + 6];
-#if VSIG_FIR_NTMID
-    // A/B: rows only this pair reads (2..11) non-temporal; the rows the
-    // neighbouring pairs share (0, 1, 12, 13) plain
-#pragma unroll
-    for (int i = 0; i < P::E / 2 + 6; ++i)
-      u[i] = (i >= 2 && i < 12) ? __builtin_nontemporal_load(b4 + t + 64 * i) : b4[t + 64 * i];
-#else
 #pragma unroll
     for (int i = 0; i < P::E / 2 + 6; ++i) u[i] = b4[t + 64 * i];   // float4 rows 0..13
-#endif
     auto unpack = [&](float2* v, int e, const f4& w) {
       const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.x), __float_as_uint(w.z), false, false);
       const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.y), __float_as_uint(w.w), false, false);

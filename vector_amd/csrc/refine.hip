@@ -96,10 +96,7 @@ static_assert(sizeof(RefineKeys) == 64, "the items follow the keys at +64 B");
 struct RefineSlot { double m; long long i; };   // one per numpy-pass block
 
 constexpr int kNpThreads = 256;
-#ifndef VSIG_NP_GRID
-#define VSIG_NP_GRID 512  // A/B: numpy-pass blocks
-#endif
-constexpr int kNpGrid = VSIG_NP_GRID;          // 2 blocks per CU (64 KB of LDS each)
+constexpr int kNpGrid = 512;                   // 2 blocks per CU (64 KB of LDS each)
 constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
 constexpr long long kBlasThreadMin = 10000;    // zdotu_k: threads only above this n
 constexpr long long kSparseMax = 4096;         // candidate outputs of the sparse form
@@ -240,25 +237,22 @@ __device__ __forceinline__ PeakPartial ld_agent(const PeakPartial* p) {
   return r;
 }
 
-// Cross-block hand-offs (a block's record, then its count on a counter): by
-// default an agent-scope fence per block (buffer_wbl2 + buffer_inv on
-// gfx950); VSIG_REFINE_RELAXED (A/B): the records as agent-scope atomic stores
-// completed (s_waitcnt) before the counter's atomic and read back with
-// agent-scope atomic loads -- no L2 write-back.
-#ifndef VSIG_REFINE_RELAXED
-#define VSIG_REFINE_RELAXED 0
+#ifndef VSIG_REFINE_TRACE
+#define VSIG_REFINE_TRACE 0  // A/B: phase timestamps (printf by the last block)
 #endif
-constexpr bool kRelaxed = VSIG_REFINE_RELAXED != 0;
-
-__device__ __forceinline__ void st_agent(PeakPartial* o, const PeakPartial& r) {
-  __hip_atomic_store(&o->max2, r.max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&o->idx, r.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&o->sum_abs, r.sum_abs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&o->sum_abs2, r.sum_abs2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+#if VSIG_REFINE_TRACE
+__device__ unsigned long long g_rt_first[2] = {~0ull, ~0ull};
+#define RT(x) const unsigned long long x = wall_clock64()
+#else
+#define RT(x)
+#endif
 
 __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) {
   const int tid = threadIdx.x;
+  RT(rt0);
+#if VSIG_REFINE_TRACE
+  if (tid == 0) atomicMin(&g_rt_first[0], rt0);
+#endif
   __shared__ int slast, ncl;
   __shared__ int clist[kFinalizeTmp];
   __shared__ double cmax[kFinalizeTmp];
@@ -276,27 +270,17 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
       s1 += p.sum_abs;
       s2 += p.sum_abs2;
     }
-    if constexpr (kRelaxed) {
-      __shared__ PeakPartial r0[1];
-      block_partial<256>(m, mi, s1, s2, r0);
-      __syncthreads();
-      if (tid == 0) st_agent(f.tmp + blockIdx.x, r0[0]);
-    } else {
-      block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
-    }
+    block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
   }
+  RT(rt1);
   if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
-    if constexpr (kRelaxed) {
-      __builtin_amdgcn_s_waitcnt(0);
-      slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
-    } else {
-      __threadfence();
-      slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
-      if (slast) __threadfence();
-    }
+    __threadfence();
+    slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
+    if (slast) __threadfence();
   }
   __syncthreads();
   if (!slast) return;
+  RT(rt2);
   const int g1 = (int)gridDim.x;
   {
     double m = -1.0, s1 = 0.0, s2 = 0.0;
@@ -325,10 +309,12 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     }
     __syncthreads();
   }
+  RT(rt3);
   const double t2 = sthr;
   for (int k = tid; k < g1; k += 256)
     if (cmax[k] >= t2) clist[atomicAdd(&ncl, 1)] = k;
   __syncthreads();
+  RT(rt4);
   // the in-band chunks' partials, a wave per 64; a wave takes each hit's 64
   // lane keys with one coalesced load and appends the in-band columns
   const int lane = tid & 63;
@@ -384,12 +370,21 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
     atomicMax(&shi, myhi);
   }
   __syncthreads();
+  RT(rt5);
   if (tid == 0) {
     RefineKeys z{};
     z.count = scount;
     z.lo_inv = ~slo;
     z.hi_p1 = shi;
     *f.keys = z;
+#if VSIG_REFINE_TRACE
+    const unsigned long long tf = g_rt_first[0];
+    g_rt_first[0] = ~0ull;
+    printf("RT fin g1=%d nc=%d items=%llu per_item=%lld | first->t0 %.2f red %.2f hand %.2f "
+           "lvl2 %.2f clist %.2f select %.2f total %.2f us\n",
+           g1, nc, scount, f.g.per_item, (rt0 - tf) * 0.01, (rt1 - rt0) * 0.01, (rt2 - rt1) * 0.01,
+           (rt3 - rt2) * 0.01, (rt4 - rt3) * 0.01, (rt5 - rt4) * 0.01, (rt5 - tf) * 0.01);
+#endif
   }
 }
 
@@ -642,6 +637,10 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
     RefineKeys* __restrict__ keys, RefineSlot* __restrict__ slots, double2* __restrict__ cv,
     double* __restrict__ vals, long long vlo, long long vhi, PeakPartial* __restrict__ rec) {
   const int tid = threadIdx.x;
+  RT(t0);
+#if VSIG_REFINE_TRACE
+  if (tid == 0) atomicMin(&g_rt_first[1], t0);
+#endif
   long long lo, hi, n;
   bool dense;
   if (vals) {
@@ -680,6 +679,7 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
   __shared__ int slast;
   __shared__ double wm[kNpThreads / 64];
   __shared__ long long wi[kNpThreads / 64];
+  RT(t1);
   double bm = -1.0;
   long long bi = 0x7fffffffffffffffLL;
   auto record = [&](long long o, double re, double im) {
@@ -710,6 +710,7 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
       if (tid == 0) record(o, re, im);
     }
   }
+  RT(t2);
   // the block's (max, lowest index), then the last block to finish reduces
   // the nact block slots (one release per block)
 #pragma unroll
@@ -725,20 +726,14 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
   __syncthreads();
   if (tid == 0) {
     for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
-    if constexpr (kRelaxed) {
-      __hip_atomic_store(&slots[blockIdx.x].m, bm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&slots[blockIdx.x].i, bi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __builtin_amdgcn_s_waitcnt(0);
-      slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
-    } else {
-      slots[blockIdx.x] = RefineSlot{bm, bi};
-      __threadfence();
-      slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
-      if (slast) __threadfence();
-    }
+    slots[blockIdx.x] = RefineSlot{bm, bi};
+    __threadfence();
+    slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
+    if (slast) __threadfence();
   }
   __syncthreads();
   if (!slast) return;
+  RT(t3);
   bm = -1.0;
   bi = 0x7fffffffffffffffLL;
   for (long long q = tid; q < nact; q += kNpThreads) {
@@ -765,6 +760,14 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
       rec->idx = bi;
     }
     keys->done = 0;
+#if VSIG_REFINE_TRACE
+    const unsigned long long tf = g_rt_first[1], t4 = wall_clock64();
+    g_rt_first[1] = ~0ull;
+    printf("RT np n=%lld dense=%d ntask=%lld nact=%lld | first->t0 %.2f keys %.2f eval %.2f "
+           "hand %.2f final %.2f total %.2f us\n",
+           n, (int)dense, ntask, nact, (t0 - tf) * 0.01, (t1 - t0) * 0.01, (t2 - t1) * 0.01,
+           (t3 - t2) * 0.01, (t4 - t3) * 0.01, (t4 - tf) * 0.01);
+#endif
   }
 }
 
