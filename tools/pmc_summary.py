@@ -19,7 +19,7 @@ from collections import defaultdict
 FAMILY = {"fir_os_kernel": "fir", "fir_dec_kernel": "fir", "fir_poly_kernel": "fir", "psd_pair_kernel": "psd",
           "psd_split_kernel": "psd", "xcorr_os_kernel": "xcorr", "xcorr_half_kernel": "xcorr",
           "pfb_kernel": "pfb", "peak_reduce": "peak", "partial_finalize": "finalize",
-          "refine_finalize_select": "finalize",
+          "refine_finalize_select": "finalize", "refine_fused": "refine", "refine_numpy": "refine",
           "refine_stage1": "refine1", "refine_stage2": "refine2", "bf_col_kernel": "bigfft_col",
           "bf_row_kernel": "bigfft_row"}
 

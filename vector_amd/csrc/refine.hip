@@ -11,9 +11,10 @@
 // This pass re-ranks every output whose fp32 |c| lies within a band eps of the
 // fp32 maximum, in numpy's own operation order and the caller's operand
 // precision (complex64 or complex128):
-//   select  : candidate items -- for the fused correlator, fused with the
-//             finalize of its wave partials into one launch (the last block
-//             to finish reduces, then selects): the thread columns whose lane
+//   select  : candidate items -- for the fused correlator, in the same launch
+//             as the finalize of its wave partials (the last block to finish
+//             reduces, then selects) and the numpy pass (refine_fused: one
+//             launch for the whole refine): the thread columns whose lane
 //             key is in the band (the outputs m(t) + TF q of one thread, where
 //             the kernel writes lane keys), else the waves whose partial max
 //             is (a wave covers ob + wstep w + l + 64 (q % rsub) + stride
@@ -53,8 +54,9 @@
 // an array (launch_refine_values: the exact confidence statistics of
 // find_correlation_peak on a flat |c|, see reduce.hip np_stats).
 // All sizes on the device (no host synchronisation).  Cross-block hand-offs
-// (last block to finish) use one agent-scope fence per block and agent-scope
-// atomic loads of what other blocks wrote.
+// (last block to finish, and refine_fused's published keys) use one
+// agent-scope fence per block and agent-scope atomic loads of what other
+// blocks wrote.
 #include "os_common.hpp"
 
 namespace vsig {
@@ -135,12 +137,14 @@ __device__ __forceinline__ long long item_output(const RefineGeom& g, long long 
   return g.rev ? g.nout - 1 - raw : raw;
 }
 
-// Candidate output e (item e / per_item, its output e % per_item), -1: none.
+// Candidate output e (item e / per_item = it, its output e % per_item), -1:
+// none; item0: items[it0] already loaded.
 __device__ __forceinline__ long long entry_output(const RefineGeom& g, const long long* items,
-                                                  long long e) {
+                                                  long long e, long long it0 = -1,
+                                                  long long item0 = 0) {
   const long long it = e / g.per_item;
   const int sub = (int)(e - it * g.per_item);
-  const long long item = items[it];
+  const long long item = it == it0 ? item0 : items[it];
   if (g.from_array) {
     const long long raw = item * 64 + sub;
     return raw < g.nout ? raw : -1;
@@ -222,7 +226,7 @@ struct FinalizeSelect {
   unsigned long long* done;         // zero between launches (reset here)
   PeakPartial* rec;                 // finalized record (max |c|)
   double eps;
-  long long* items; RefineKeys* keys;
+  long long* items; long long maxitems; RefineKeys* keys;
   const unsigned* lkeys;            // optional lane keys (64 per wave partial)
   RefineGeom g;                     // item -> output spans
 };
@@ -242,12 +246,15 @@ __device__ __forceinline__ PeakPartial ld_agent(const PeakPartial* p) {
 #endif
 #if VSIG_REFINE_TRACE
 __device__ unsigned long long g_rt_first[2] = {~0ull, ~0ull};
+__shared__ unsigned long long g_rtz[8];       // np_zdot_chunk / phase-A sub-steps (thread 0)
 #define RT(x) const unsigned long long x = wall_clock64()
 #else
 #define RT(x)
 #endif
 
-__global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) {
+// Block vb of g1 (first-level chunk vb); true for the block that finished
+// last, after it has reduced, selected and written the keys.
+__device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, int vb, int g1) {
   const int tid = threadIdx.x;
   RT(rt0);
 #if VSIG_REFINE_TRACE
@@ -259,29 +266,41 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
   __shared__ unsigned long long scount, slo, shi;
   __shared__ double sthr;
   {
-    const long long lo = (long long)blockIdx.x * f.chunk;
+    const long long lo = (long long)vb * f.chunk;
     const long long hi = lo + f.chunk < f.nparts ? lo + f.chunk : f.nparts;
     double m = -1.0, s1 = 0.0, s2 = 0.0;
     long long mi = 0x7fffffffffffffffLL;
-#pragma unroll 8
-    for (long long i = lo + tid; i < hi; i += 256) {
-      const PeakPartial p = f.parts[i];
-      betterd(m, mi, p.max2, p.idx);
-      s1 += p.sum_abs;
-      s2 += p.sum_abs2;
+    constexpr int kL = 4;                       // loads in flight per thread
+    for (long long i0 = lo + tid; i0 < hi; i0 += 256 * kL) {   // a thread's partials in order
+      PeakPartial p[kL];
+#pragma unroll
+      for (int q = 0; q < kL; ++q) {
+        const long long i = i0 + 256LL * q;
+        if (i < hi) p[q] = f.parts[i];
+      }
+#pragma unroll
+      for (int q = 0; q < kL; ++q) {
+        if (i0 + 256LL * q < hi) {
+          betterd(m, mi, p[q].max2, p[q].idx);
+          s1 += p[q].sum_abs;
+          s2 += p[q].sum_abs2;
+        }
+      }
     }
-    block_partial<256>(m, mi, s1, s2, f.tmp + blockIdx.x);   // thread 0 writes
+#if VSIG_REFINE_TRACE
+    if (tid == 0) g_rtz[5] = wall_clock64();
+#endif
+    block_partial<256>(m, mi, s1, s2, f.tmp + vb);   // thread 0 writes
   }
   RT(rt1);
   if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
     __threadfence();
-    slast = atomicAdd(f.done, 1ull) == (unsigned long long)gridDim.x - 1;
+    slast = atomicAdd(f.done, 1ull) == (unsigned long long)g1 - 1;
     if (slast) __threadfence();
   }
   __syncthreads();
-  if (!slast) return;
+  if (!slast) return false;
   RT(rt2);
-  const int g1 = (int)gridDim.x;
   {
     double m = -1.0, s1 = 0.0, s2 = 0.0;
     long long mi = 0x7fffffffffffffffLL;
@@ -380,50 +399,51 @@ __global__ __launch_bounds__(256) void refine_finalize_select(FinalizeSelect f) 
 #if VSIG_REFINE_TRACE
     const unsigned long long tf = g_rt_first[0];
     g_rt_first[0] = ~0ull;
-    printf("RT fin g1=%d nc=%d items=%llu per_item=%lld | first->t0 %.2f red %.2f hand %.2f "
+    printf("RT fin g1=%d nc=%d items=%llu per_item=%lld | first->t0 %.2f loads %.2f hand %.2f "
            "lvl2 %.2f clist %.2f select %.2f total %.2f us\n",
-           g1, nc, scount, f.g.per_item, (rt0 - tf) * 0.01, (rt1 - rt0) * 0.01, (rt2 - rt1) * 0.01,
+           g1, nc, scount, f.g.per_item, (rt0 - tf) * 0.01, (g_rtz[5] - rt0) * 0.01, (rt2 - rt1) * 0.01,
            (rt3 - rt2) * 0.01, (rt4 - rt3) * 0.01, (rt5 - rt4) * 0.01, (rt5 - tf) * 0.01);
 #endif
   }
+  return true;
 }
 
 // One zdot_compute over chunk [c0, c0 + w) of output i's overlap (x = a +
 // ax, y = conj(v)), in numpy's order.  Tiles of kTile complex are staged by
-// the whole block into LDS as planar doubles (xr, xi, yr, -yi); lane
-// 8 comp + s (< 32) of wave 0 runs one of zdot_kernel_8's fma chains: slot s
-// (complex k = s mod 8 of the block part n8 = w & -8) of component comp (xr yr,
-// xi yi, xr yi, xi yr) -- one dependent fma per step, its operands two LDS
-// reads.  The add tree combines the slots as the kernel does ((s, s^2), then
-// (s, s^4), then the two 128-bit halves: s, s^1); lane 0 gathers the four
-// sums and runs the scalar tail.  Result in lane 0.
+// the whole block into LDS as complex doubles (x, and y as (yr, -yi)); lane s
+// (< 8) of wave 0 runs the four fma chains of zdot_kernel_8's slot s
+// (complex k = s mod 8 of the block part n8 = w & -8), one per component (xr
+// yr, xi yi, xr yi, xi yr): four independent fmas per step from two 16-byte
+// LDS reads, read a batch of kB steps ahead, so a step costs the fma latency
+// (15 clocks on gfx950) rather than an LDS round trip.  The add tree combines
+// the slots as the kernel does ((s, s^2), then (s, s^4), then the two 128-bit
+// halves: s, s^1); lane 0 runs the scalar tail.  Result in lane 0.
 template <class T>
 __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* __restrict__ v,
                                               long long ax, long long c0, long long w,
                                               double* lds, double& re, double& im) {
-  const int tid = threadIdx.x, s = tid & 7, comp = (tid >> 3) & 3;
-  double* xr = lds;
-  double* xi = lds + kTile;
-  double* yr = lds + 2 * kTile;
-  double* yn = lds + 3 * kTile;
-  const double* X = (comp == 0 || comp == 2) ? xr : xi;
-  const double* Y = (comp == 0 || comp == 3) ? yr : yn;
+  const int tid = threadIdx.x, s = tid & 7;
+  double2* xs = reinterpret_cast<double2*>(lds);
+  double2* ys = xs + kTile;
   const long long n8 = w & ~7LL;
-  double acc = 0.0;
+  double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
   // tile t + 1's loads are in flight (registers) while the chains run over
   // tile t (LDS)
   constexpr int kPer = kTile / kNpThreads;
-  T xs[kPer], ys[kPer];
+  T xg[kPer], yg[kPer];
   auto fetch = [&](long long tb) {
     const int tl = n8 - tb < kTile ? (int)(n8 - tb) : kTile;
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int j = tid + q * kNpThreads;
       const bool in = j < tl;
-      xs[q] = in ? a[ax + c0 + tb + j] : T{};
-      ys[q] = in ? v[c0 + tb + j] : T{};
+      xg[q] = in ? a[ax + c0 + tb + j] : T{};
+      yg[q] = in ? v[c0 + tb + j] : T{};
     }
   };
+#if VSIG_REFINE_TRACE
+  if (tid == 0) g_rtz[0] = wall_clock64();
+#endif
   if (n8 > 0) fetch(0);
   for (long long tb = 0; tb < n8; tb += kTile) {  // uniform
     const int tl = n8 - tb < kTile ? (int)(n8 - tb) : kTile;
@@ -431,39 +451,85 @@ __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* 
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int j = tid + q * kNpThreads;
-      xr[j] = (double)xs[q].x;
-      xi[j] = (double)xs[q].y;
-      yr[j] = (double)ys[q].x;
-      yn[j] = -(double)ys[q].y;
+      xs[j] = to_d2(xg[q]);
+      const double2 y = to_d2(yg[q]);
+      ys[j] = make_double2(y.x, -y.y);
     }
     __syncthreads();
+#if VSIG_REFINE_TRACE
+    if (tid == 0 && tb == 0) { g_rtz[1] = wall_clock64(); g_rtz[6] = clock64(); }
+#endif
     if (tb + kTile < n8) fetch(tb + kTile);
-    if (tid < 32) {
-#pragma unroll 16
-      for (int k = s; k < tl; k += 8) acc = fma(X[k], Y[k], acc);
+    if (tid < 8) {
+      constexpr int kB = 4;
+      const double2* Xs = xs + s;
+      const double2* Ys = ys + s;
+      const int nst = tl >> 3;                    // steps of this tile (tl % 8 == 0)
+      const int nfull = nst & ~(kB - 1);
+      auto step = [&](const double2& x, const double2& y) {
+        d0 = fma(x.x, y.x, d0);
+        d1 = fma(x.y, y.y, d1);
+        d2 = fma(x.x, y.y, d2);
+        d3 = fma(x.y, y.x, d3);
+      };
+      double2 xb[kB], yb[kB];
+      if (nfull > 0) {
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+          xb[i] = Xs[8 * i];
+          yb[i] = Ys[8 * i];
+        }
+      }
+      for (int j = 0; j < nfull; j += kB) {      // uniform
+        double2 xn[kB], yn[kB];
+        const int jn = j + kB < nfull ? j + kB : j;   // the last batch re-reads its own
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+          xn[i] = Xs[8 * (jn + i)];
+          yn[i] = Ys[8 * (jn + i)];
+        }
+#pragma unroll
+        for (int i = 0; i < kB; ++i) step(xb[i], yb[i]);
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+          xb[i] = xn[i];
+          yb[i] = yn[i];
+        }
+      }
+      for (int j = nfull; j < nst; ++j) step(Xs[8 * j], Ys[8 * j]);
     }
+#if VSIG_REFINE_TRACE
+    if (tid == 0) g_rtz[tb == 0 ? 2 : 3] = wall_clock64() + 0 * (unsigned long long)__double_as_longlong(d0);
+    if (tid == 0 && tb == 0) g_rtz[7] = clock64() + 0 * (unsigned long long)__double_as_longlong(d0);
+#endif
   }
-  if (tid < 32) {                                 // lanes 0..31 of wave 0
-    acc = acc + __shfl_xor(acc, 2, 8);
-    acc = acc + __shfl_xor(acc, 4, 8);
-    acc = acc + __shfl_xor(acc, 1, 8);            // lane 8 comp: d_comp
-    double d0 = acc;
-    const double d1 = __shfl(acc, 8), d2s = __shfl(acc, 16), d3s = __shfl(acc, 24);
+  if (tid < 8) {                                  // lanes 0..7 of wave 0
+    auto tree = [](double u) {
+      u = u + __shfl_xor(u, 2, 8);
+      u = u + __shfl_xor(u, 4, 8);
+      return u + __shfl_xor(u, 1, 8);
+    };
+    d0 = tree(d0);
+    d1 = tree(d1);
+    d2 = tree(d2);
+    d3 = tree(d3);
     if (tid == 0) {
-      double d1t = d1, d2 = d2s, d3 = d3s;
       for (long long t = n8; t < w; ++t) {
         const double2 x = ld2<T>(a, ax + c0 + t), y = ld2<T>(v, c0 + t);
         const double yi = -y.y;
         d0 = fma(x.x, y.x, d0);
-        d1t = fma(x.y, yi, d1t);
+        d1 = fma(x.y, yi, d1);
         d2 = fma(x.x, yi, d2);
         d3 = fma(y.x, x.y, d3);
       }
-      double r = d0 - d1t;
+      double r = d0 - d1;
       const double m = d2 + d3;
       r = fma(m, 0.0, r);
       re = r;
       im = m;
+#if VSIG_REFINE_TRACE
+      g_rtz[4] = wall_clock64() + 0 * (unsigned long long)__double_as_longlong(r);
+#endif
     }
   }
 }
@@ -627,20 +693,26 @@ __device__ __forceinline__ void eval_group(const T* __restrict__ a, const T* __r
   im_out = 0.0 + im;
 }
 
-// The numpy pass.  Candidate mode (vals == nullptr): the select's items;
+// The numpy pass of virtual block vb of nb.  Candidate mode (vals ==
+// nullptr): the select's cnt items spanning outputs [~lo_inv, hi_p1 - 1];
 // values mode: every output of [vlo, vhi], |c| into vals[o - vlo].  Every
 // evaluated output updates the block's (max |c|, lowest index); the last block
-// to finish writes numpy's argmax into rec.
+// to finish writes numpy's argmax into rec.  nact: blocks that take part (the
+// others return at once); true for the block that finished last.
 template <class T>
-__global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
-    const T* __restrict__ a, const T* __restrict__ v, RefineGeom g, const long long* __restrict__ items,
-    RefineKeys* __restrict__ keys, RefineSlot* __restrict__ slots, double2* __restrict__ cv,
-    double* __restrict__ vals, long long vlo, long long vhi, PeakPartial* __restrict__ rec) {
+__device__ __forceinline__ bool numpy_pass(
+    const T* __restrict__ a, const T* __restrict__ v, const RefineGeom& g,
+    const long long* __restrict__ items, RefineKeys* __restrict__ keys, RefineSlot* __restrict__ slots,
+    double2* __restrict__ cv, double* __restrict__ vals, long long vlo, long long vhi,
+    PeakPartial* __restrict__ rec, unsigned long long cnt, unsigned long long lo_inv,
+    unsigned long long hi_p1, long long vb, long long nb, long long& nact, long long it0 = -1,
+    long long item0 = 0) {
   const int tid = threadIdx.x;
   RT(t0);
 #if VSIG_REFINE_TRACE
   if (tid == 0) atomicMin(&g_rt_first[1], t0);
 #endif
+  nact = 0;
   long long lo, hi, n;
   bool dense;
   if (vals) {
@@ -649,15 +721,14 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
     n = hi - lo + 1;
     dense = true;
   } else {
-    const long long cnt = (long long)keys->count;
-    if (cnt == 0) return;                          // uniform: no block counts itself
-    n = cnt * g.per_item;
+    if (cnt == 0) return false;                    // uniform: no block counts itself
+    n = (long long)cnt * g.per_item;
     if (g.cap > 0 && n > g.cap) {                  // opt-in limit: record left fp32
-      if (blockIdx.x == 0 && tid == 0) keys->status = 1;
-      return;
+      if (vb == 0 && tid == 0) keys->status = 1;
+      return false;
     }
-    lo = (long long)~keys->lo_inv;
-    hi = (long long)keys->hi_p1 - 1;
+    lo = (long long)~lo_inv;
+    hi = (long long)hi_p1 - 1;
     dense = n > kSparseMax && hi - lo + 1 <= 8 * n;
   }
   // full-overlap (interior) outputs of the span
@@ -673,8 +744,8 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
   const long long ntask = dense ? ngroups + nleft + nright : n;
   // blocks past the task count take no part (the last-block hand-off counts
   // only the nact blocks that have work)
-  const long long nact = ntask < (long long)gridDim.x ? ntask : (long long)gridDim.x;
-  if ((long long)blockIdx.x >= nact) return;
+  nact = ntask < nb ? ntask : nb;
+  if (vb >= nact) return false;
   __shared__ double tiles[4 * kTile];
   __shared__ int slast;
   __shared__ double wm[kNpThreads / 64];
@@ -688,7 +759,7 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
     if (cv) cv[o] = make_double2(re, im);
     if (vals) vals[o - lo] = av;
   };
-  for (long long t = blockIdx.x; t < ntask; t += gridDim.x) {   // uniform per block
+  for (long long t = vb; t < ntask; t += nb) {     // uniform per block
     if (dense && t < ngroups) {
       const long long ob = ilo + 256 * t + 64 * (tid >> 6);
       double re, im;
@@ -702,7 +773,7 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
         const long long e = t - ngroups;
         o = e < nleft ? lo + e : ihi + 1 + (e - nleft);
       } else {
-        o = entry_output(g, items, t);
+        o = entry_output(g, items, t, it0, item0);
         if (o < 0) continue;
       }
       double re, im;
@@ -726,13 +797,13 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
   __syncthreads();
   if (tid == 0) {
     for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
-    slots[blockIdx.x] = RefineSlot{bm, bi};
+    slots[vb] = RefineSlot{bm, bi};
     __threadfence();
     slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
     if (slast) __threadfence();
   }
   __syncthreads();
-  if (!slast) return;
+  if (!slast) return false;
   RT(t3);
   bm = -1.0;
   bi = 0x7fffffffffffffffLL;
@@ -763,11 +834,107 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
 #if VSIG_REFINE_TRACE
     const unsigned long long tf = g_rt_first[1], t4 = wall_clock64();
     g_rt_first[1] = ~0ull;
-    printf("RT np n=%lld dense=%d ntask=%lld nact=%lld | first->t0 %.2f keys %.2f eval %.2f "
-           "hand %.2f final %.2f total %.2f us\n",
+    printf("RT np n=%lld dense=%d ntask=%lld nact=%lld | first->t0 %.2f setup %.2f eval %.2f "
+           "[pre %.2f fetch0 %.2f chain0 %.2f (%.0f clk/step, %.2f GHz) chain1 %.2f tail %.2f] hand %.2f final %.2f total %.2f us\n",
            n, (int)dense, ntask, nact, (t0 - tf) * 0.01, (t1 - t0) * 0.01, (t2 - t1) * 0.01,
+           ((long long)g_rtz[0] - (long long)t1) * 0.01, ((long long)g_rtz[1] - (long long)g_rtz[0]) * 0.01,
+           ((long long)g_rtz[2] - (long long)g_rtz[1]) * 0.01,
+           (double)((long long)g_rtz[7] - (long long)g_rtz[6]) / 256.0,
+           (double)((long long)g_rtz[7] - (long long)g_rtz[6]) / ((double)((long long)g_rtz[2] - (long long)g_rtz[1]) * 10.0),
+           ((long long)g_rtz[3] - (long long)g_rtz[2]) * 0.01,
+           ((long long)g_rtz[4] - (long long)g_rtz[3]) * 0.01,
            (t3 - t2) * 0.01, (t4 - t3) * 0.01, (t4 - tf) * 0.01);
 #endif
+  }
+  return true;
+}
+
+// The numpy pass as a launch of its own: values mode, and candidates selected
+// from a stored c64 array (refine_select_array).
+template <class T>
+__global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
+    const T* __restrict__ a, const T* __restrict__ v, RefineGeom g, const long long* __restrict__ items,
+    RefineKeys* __restrict__ keys, RefineSlot* __restrict__ slots, double2* __restrict__ cv,
+    double* __restrict__ vals, long long vlo, long long vhi, PeakPartial* __restrict__ rec) {
+  unsigned long long cnt = 0, lo_inv = 0, hi_p1 = 0;
+  if (!vals) {
+    cnt = keys->count;
+    lo_inv = keys->lo_inv;
+    hi_p1 = keys->hi_p1;
+  }
+  long long nact;
+  (void)numpy_pass<T>(a, v, g, items, keys, slots, cv, vals, vlo, vhi, rec, cnt, lo_inv, hi_p1,
+                      blockIdx.x, gridDim.x, nact);
+}
+
+// The fused correlator's whole refine in one launch: g1 finalize / select
+// blocks, then kNpGrid numpy blocks.  Blocks take tickets in the order they
+// start; tickets < g1 run finalize_select_block and exit (the last one
+// publishes the keys with a flag), tickets >= g1 wait for the flag and run the
+// numpy pass.  A numpy block only ever waits for blocks that started before
+// it and never wait themselves, so the launch finishes whatever the residency
+// (no co-residency assumption, other kernels may share the CUs).  The four
+// counters (zero between launches) are reset by the last numpy block once
+// every numpy block has read the keys.
+struct FusedCounters {
+  unsigned long long done_a;   // FinalizeSelect::done (first-level blocks finished)
+  unsigned long long ticket;   // blocks started
+  unsigned long long seen;     // numpy blocks that have read the keys
+  unsigned long long pad0[5];
+  unsigned long long flag;     // 1: keys and items published (own 64-byte line: polled)
+  unsigned long long pad1[7];
+};
+static_assert(sizeof(FusedCounters) == kCounterRecs * sizeof(PeakPartial), "counter slots");
+
+template <class T>
+__global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
+    FinalizeSelect f, int g1, const T* __restrict__ a, const T* __restrict__ v,
+    RefineSlot* __restrict__ slots, double2* __restrict__ cv) {
+  FusedCounters* fc = reinterpret_cast<FusedCounters*>(f.done);
+  const int tid = threadIdx.x;
+  __shared__ long long stk, sitem0;
+  __shared__ unsigned long long skeys[3];
+  if (tid == 0) stk = (long long)atomicAdd(&fc->ticket, 1ull);
+  __syncthreads();
+  const long long tk = stk;
+  if (tk < g1) {
+    if (finalize_select_block(f, (int)tk, g1) && tid == 0) {
+      __threadfence();                             // keys + items, then the flag
+      __hip_atomic_store(&fc->flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  const long long vb = tk - g1;
+  // the item of this block's first task in the sparse form, read with the keys
+  const long long it0 = vb / f.g.per_item;
+  if (tid == 0) {
+    // the first 64 numpy blocks poll every ~1300 clocks (the usual handful of
+    // candidates), the rest every ~8000 (they matter only for a dense pass);
+    // one 64-byte line holds the flag alone
+    while (__hip_atomic_load(&fc->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (vb < 64) __builtin_amdgcn_s_sleep(20);
+      else __builtin_amdgcn_s_sleep(127);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    skeys[0] = __hip_atomic_load(&f.keys->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    skeys[1] = __hip_atomic_load(&f.keys->lo_inv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    skeys[2] = __hip_atomic_load(&f.keys->hi_p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sitem0 = it0 < f.maxitems
+                 ? __hip_atomic_load(&f.items[it0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                 : 0;
+    atomicAdd(&fc->seen, 1ull);
+  }
+  __syncthreads();
+  long long nact;
+  const bool last = numpy_pass<T>(a, v, f.g, f.items, f.keys, slots, cv, nullptr, 0, 0, f.rec,
+                                  skeys[0], skeys[1], skeys[2], vb, kNpGrid, nact,
+                                  (unsigned long long)it0 < skeys[0] ? it0 : -1, sitem0);
+  if (tid == 0 && (last || (nact == 0 && vb == 0))) {
+    while (__hip_atomic_load(&fc->seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)kNpGrid)
+      __builtin_amdgcn_s_sleep(20);
+    __hip_atomic_store(&fc->seen, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&fc->flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&fc->ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -808,7 +975,7 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
   long long* items = reinterpret_cast<long long*>(base + sizeof(RefineKeys));
   RefineSlot* slots = reinterpret_cast<RefineSlot*>(items + max_items(r));
   const RefineGeom g = make_geom(r);
-  if (r.finalize) {              // the partials' finalize + select in one launch
+  if (r.finalize) {              // the partials' finalize + select + numpy pass in one launch
     if (r.from_array || !r.tmp || !r.done) return hipErrorInvalidValue;
     constexpr long long kFinChunk = 1024;   // wave partials per first-level block
     long long g1 = (r.nparts + kFinChunk - 1) / kFinChunk;
@@ -818,19 +985,26 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
     if (chunk < 1) chunk = 1;
     g1 = (r.nparts + chunk - 1) / chunk;
     if (g1 < 1) g1 = 1;
-    const FinalizeSelect f{r.parts, r.nparts, chunk, r.tmp, r.done, r.rec, r.eps, items, keys,
-                           r.lkeys, g};
-    hipLaunchKernelGGL(refine_finalize_select, dim3((unsigned)g1), dim3(256), 0, st, f);
-  } else {
-    // a stored c64 array (the correlator's partials are finalized and
-    // selected by refine_finalize_select above)
-    if (r.cols || r.lkeys || !r.from_array) return hipErrorInvalidValue;
-    hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
-    if (e != hipSuccess) return e;
-    const long long grid = (r.nout + 255) / 256;
-    hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
-                       r.rec, r.eps, items, keys);
+    const FinalizeSelect f{r.parts, r.nparts, chunk, r.tmp, r.done, r.rec, r.eps, items,
+                           max_items(r), keys, r.lkeys, g};
+    const dim3 grid((unsigned)(g1 + kNpGrid));
+    if (r.c128)
+      hipLaunchKernelGGL(refine_fused<double2>, grid, dim3(kNpThreads), 0, st, f, (int)g1,
+                         static_cast<const double2*>(r.a), static_cast<const double2*>(r.v), slots,
+                         static_cast<double2*>(r.out128));
+    else
+      hipLaunchKernelGGL(refine_fused<float2>, grid, dim3(kNpThreads), 0, st, f, (int)g1,
+                         static_cast<const float2*>(r.a), static_cast<const float2*>(r.v), slots,
+                         static_cast<double2*>(r.out128));
+    return hipGetLastError();
   }
+  // a stored c64 array: keys memset, select, numpy pass
+  if (r.cols || r.lkeys || !r.from_array) return hipErrorInvalidValue;
+  hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
+  if (e != hipSuccess) return e;
+  const long long grid = (r.nout + 255) / 256;
+  hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,
+                     r.rec, r.eps, items, keys);
   return launch_numpy(r, g, items, keys, slots, nullptr, 0, 0, st);
 }
 

@@ -177,8 +177,8 @@ int ensure_partials(vsig_ctx* c, long long n) {
   long long cap = n < 4096 ? 4096 : n + n / 4;
   // + the first-level buffer of a two-level finalize, right after the partials,
   // and the fused finalize's block counter (zero between launches)
-  HIPCHK(c, hipMalloc(&c->partials, (cap + vsig::kFinalizeTmp + 1) * sizeof(PeakPartial)));
-  HIPCHK(c, hipMemset(c->partials + cap + vsig::kFinalizeTmp, 0, sizeof(PeakPartial)));
+  HIPCHK(c, hipMalloc(&c->partials, (cap + vsig::kFinalizeTmp + vsig::kCounterRecs) * sizeof(PeakPartial)));
+  HIPCHK(c, hipMemset(c->partials + cap + vsig::kFinalizeTmp, 0, vsig::kCounterRecs * sizeof(PeakPartial)));
   c->npartials = cap;
   return VSIG_OK;
 }

@@ -139,6 +139,9 @@ hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int varian
 hipError_t launch_peak_reduce(int dtype, const void* a, long long n, PeakPartial* partials,
                               int nparts, hipStream_t st);
 constexpr int kFinalizeTmp = 1024;   // first-level partials of a two-level finalize
+// zeroed PeakPartial-sized slots after the kFinalizeTmp records: the
+// finalize's counter (first 8 B) and refine_fused's counters (128 B)
+constexpr int kCounterRecs = 4;
 hipError_t launch_partial_finalize(const PeakPartial* parts, long long nparts, int sqrt_max,
                                    PeakPartial* out, PeakPartial* tmp, hipStream_t st);
 
@@ -161,7 +164,8 @@ struct RefineArgs {
   const unsigned* lkeys;            //   cols rows each), lkeys: 64 per wave partial
   int finalize;                     // finalize the partials here (+ select, one launch):
   PeakPartial* tmp;                 //   kFinalizeTmp first-level records,
-  unsigned long long* done;         //   a counter that is zero between launches
+  unsigned long long* done;         //   kCounterRecs records' worth of counters,
+                                    //   zero between launches
   long long cap;                    // opt-in limit on candidate outputs (0: none)
   void* scratch;                    // refine_scratch_bytes(*this)
   PeakPartial* rec;                 // finalized record (max |c|), updated in place
