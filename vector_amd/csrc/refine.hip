@@ -74,6 +74,21 @@ template <> __device__ __forceinline__ double2 ld2<double2>(const double2* p, lo
 __device__ __forceinline__ double2 to_d2(float2 v) { return make_double2((double)v.x, (double)v.y); }
 __device__ __forceinline__ double2 to_d2(double2 v) { return v; }
 
+template <class U>
+__device__ __forceinline__ void st_agent(U* p, U v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class U>
+__device__ __forceinline__ U ld_agent(const U* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// The cross-block hand-offs: what a block hands over is written with
+// agent-scope atomic stores (coherent across the XCDs' L2s) and completed
+// (s_waitcnt: the stores acknowledged) before the counter's atomic or the
+// flag; readers use agent-scope atomic loads.  No L2 write-back fence
+// (buffer_wbl2 costs microseconds behind the correlator's dirty lines).
+__device__ __forceinline__ void stores_done() { __builtin_amdgcn_s_waitcnt(0); }
+
 // Overlap of output i (index into the 'full' correlation) with a: taps
 // k in [k0, k1), a index i - (nv - 1) + k.
 __device__ __forceinline__ void tap_range(long long i, long long na, long long nv, long long& k0,
@@ -100,6 +115,7 @@ struct RefineSlot { double m; long long i; };   // one per numpy-pass block
 constexpr int kNpThreads = 256;
 constexpr int kNpGrid = 512;                   // 2 blocks per CU (64 KB of LDS each)
 constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
+constexpr int kTilePad = 8;                    // doubles: 64 B = 16 LDS banks
 constexpr long long kBlasThreadMin = 10000;    // zdotu_k: threads only above this n
 constexpr long long kSparseMax = 4096;         // candidate outputs of the sparse form
 
@@ -144,7 +160,7 @@ __device__ __forceinline__ long long entry_output(const RefineGeom& g, const lon
                                                   long long item0 = 0) {
   const long long it = e / g.per_item;
   const int sub = (int)(e - it * g.per_item);
-  const long long item = it == it0 ? item0 : items[it];
+  const long long item = it == it0 ? item0 : ld_agent(items + it);
   if (g.from_array) {
     const long long raw = item * 64 + sub;
     return raw < g.nout ? raw : -1;
@@ -241,6 +257,13 @@ __device__ __forceinline__ PeakPartial ld_agent(const PeakPartial* p) {
   return r;
 }
 
+__device__ __forceinline__ void st_agent(PeakPartial* o, const PeakPartial& r) {
+  __hip_atomic_store(&o->max2, r.max2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->idx, r.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->sum_abs, r.sum_abs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->sum_abs2, r.sum_abs2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 #ifndef VSIG_REFINE_TRACE
 #define VSIG_REFINE_TRACE 0  // A/B: phase timestamps (printf by the last block)
 #endif
@@ -290,13 +313,15 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
 #if VSIG_REFINE_TRACE
     if (tid == 0) g_rtz[5] = wall_clock64();
 #endif
-    block_partial<256>(m, mi, s1, s2, f.tmp + vb);   // thread 0 writes
+    __shared__ PeakPartial r0[1];
+    block_partial<256>(m, mi, s1, s2, r0);
+    __syncthreads();
+    if (tid == 0) st_agent(f.tmp + vb, r0[0]);
   }
   RT(rt1);
-  if (tid == 0) {      // one release per block (an agent-scope fence writes L2 back)
-    __threadfence();
+  if (tid == 0) {
+    stores_done();
     slast = atomicAdd(f.done, 1ull) == (unsigned long long)g1 - 1;
-    if (slast) __threadfence();
   }
   __syncthreads();
   if (!slast) return false;
@@ -317,10 +342,10 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
     if (tid == 0) {
       PeakPartial o = r[0];
       o.max2 = sqrt(o.max2);
-      *f.rec = o;
+      st_agent(f.rec, o);
       const double t = o.max2 * (1.0 - f.eps);
       sthr = t > 0.0 ? t * t : 0.0;                // partials hold fp32 |c|^2
-      *f.done = 0;
+      st_agent(f.done, 0ull);
       ncl = 0;
       scount = 0;
       slo = ~0ull;
@@ -373,7 +398,7 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
           j0 = __shfl(j0, 0);
           const unsigned long long j = j0 + __popcll(km & ((1ull << lane) - 1));
           if (take) {
-            f.items[j] = item;
+            st_agent(f.items + j, item);
             long long ilo, ihi;
             if (item_span(f.g, item, ilo, ihi)) {
               mylo = (unsigned long long)ilo < mylo ? (unsigned long long)ilo : mylo;
@@ -388,14 +413,18 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
     atomicMin(&slo, mylo);
     atomicMax(&shi, myhi);
   }
-  __syncthreads();
+  __syncthreads();                                // the totals in LDS
   RT(rt5);
   if (tid == 0) {
-    RefineKeys z{};
-    z.count = scount;
-    z.lo_inv = ~slo;
-    z.hi_p1 = shi;
-    *f.keys = z;
+    st_agent(&f.keys->count, scount);
+    st_agent(&f.keys->lo_inv, ~slo);
+    st_agent(&f.keys->hi_p1, shi);
+    st_agent(&f.keys->status, 0ull);
+    st_agent(&f.keys->done, 0ull);
+  }
+  stores_done();                                  // this thread's items (thread 0: the keys)
+  __syncthreads();                                // ... all complete before the caller's flag
+  if (tid == 0) {
 #if VSIG_REFINE_TRACE
     const unsigned long long tf = g_rt_first[0];
     g_rt_first[0] = ~0ull;
@@ -410,23 +439,33 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
 
 // One zdot_compute over chunk [c0, c0 + w) of output i's overlap (x = a +
 // ax, y = conj(v)), in numpy's order.  Tiles of kTile complex are staged by
-// the whole block into LDS as complex doubles (x, and y as (yr, -yi)); lane s
-// (< 8) of wave 0 runs the four fma chains of zdot_kernel_8's slot s
-// (complex k = s mod 8 of the block part n8 = w & -8), one per component (xr
-// yr, xi yi, xr yi, xi yr): four independent fmas per step from two 16-byte
-// LDS reads, read a batch of kB steps ahead, so a step costs the fma latency
-// (15 clocks on gfx950) rather than an LDS round trip.  The add tree combines
-// the slots as the kernel does ((s, s^2), then (s, s^4), then the two 128-bit
-// halves: s, s^1); lane 0 runs the scalar tail.  Result in lane 0.
+// the whole block into LDS as planar doubles (xr, xi, yr, -yi); lane
+// 8 comp + s (< 32) of wave 0 runs one of zdot_kernel_8's fma chains: slot s
+// (complex k = s mod 8 of the block part n8 = w & -8) of component comp (xr yr,
+// xi yi, xr yi, xi yr) -- one dependent fma per step (one wave instruction
+// for all 32 chains), its operands read a batch of kB steps ahead.  Measured
+// (tools/probes/fma_lat.hip): 15 clocks per dependent fp64 fma, ~25 per step
+// of this loop; four chains per lane (8 lanes) run at ~50.  The add tree
+// combines the slots as the kernel does ((s, s^2), then (s, s^4), then the two
+// 128-bit halves: s, s^1); lane 0 gathers the four sums and runs the scalar
+// tail.  Result in lane 0.
 template <class T>
 __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* __restrict__ v,
                                               long long ax, long long c0, long long w,
                                               double* lds, double& re, double& im) {
-  const int tid = threadIdx.x, s = tid & 7;
-  double2* xs = reinterpret_cast<double2*>(lds);
-  double2* ys = xs + kTile;
+  const int tid = threadIdx.x, s = tid & 7, comp = (tid >> 3) & 3;
+  // xi and yn start 16 banks (64 B) off xr's / yr's bank alignment: a step's
+  // read serves components 0 / 2 from xr and 1 / 3 from xi (and 0 / 3 from
+  // yr, 1 / 2 from yn) in one instruction, which would otherwise meet on the
+  // same banks (2-way conflicts: 46 instead of ~25 clocks per step)
+  double* xr = lds;
+  double* xi = lds + kTile + kTilePad;
+  double* yr = lds + 2 * kTile + 2 * kTilePad;
+  double* yn = lds + 3 * kTile + 3 * kTilePad;
+  const double* X = (comp == 0 || comp == 2) ? xr : xi;
+  const double* Y = (comp == 0 || comp == 3) ? yr : yn;
   const long long n8 = w & ~7LL;
-  double d0 = 0.0, d1 = 0.0, d2 = 0.0, d3 = 0.0;
+  double acc = 0.0;
   // tile t + 1's loads are in flight (registers) while the chains run over
   // tile t (LDS)
   constexpr int kPer = kTile / kNpThreads;
@@ -451,78 +490,74 @@ __device__ __forceinline__ void np_zdot_chunk(const T* __restrict__ a, const T* 
 #pragma unroll
     for (int q = 0; q < kPer; ++q) {
       const int j = tid + q * kNpThreads;
-      xs[j] = to_d2(xg[q]);
-      const double2 y = to_d2(yg[q]);
-      ys[j] = make_double2(y.x, -y.y);
+      xr[j] = (double)xg[q].x;
+      xi[j] = (double)xg[q].y;
+      yr[j] = (double)yg[q].x;
+      yn[j] = -(double)yg[q].y;
     }
     __syncthreads();
 #if VSIG_REFINE_TRACE
     if (tid == 0 && tb == 0) { g_rtz[1] = wall_clock64(); g_rtz[6] = clock64(); }
 #endif
     if (tb + kTile < n8) fetch(tb + kTile);
-    if (tid < 8) {
-      constexpr int kB = 4;
-      const double2* Xs = xs + s;
-      const double2* Ys = ys + s;
+    if (tid < 32) {
+      // two register batches of kB steps in turn: batch B's reads are in
+      // flight while batch A's fmas run and vice versa (no register copies
+      // between the reads and the fmas)
+      constexpr int kB = 8;
+      const double* Xs = X + s;
+      const double* Ys = Y + s;
       const int nst = tl >> 3;                    // steps of this tile (tl % 8 == 0)
-      const int nfull = nst & ~(kB - 1);
-      auto step = [&](const double2& x, const double2& y) {
-        d0 = fma(x.x, y.x, d0);
-        d1 = fma(x.y, y.y, d1);
-        d2 = fma(x.x, y.y, d2);
-        d3 = fma(x.y, y.x, d3);
+      const int nfull = nst & ~(2 * kB - 1);
+      double xa[kB], ya[kB], xb[kB], yb[kB];
+      auto rd = [&](double* xv, double* yv, int j) {
+#pragma unroll
+        for (int i = 0; i < kB; ++i) {
+          xv[i] = Xs[8 * (j + i)];
+          yv[i] = Ys[8 * (j + i)];
+        }
       };
-      double2 xb[kB], yb[kB];
-      if (nfull > 0) {
+      auto run = [&](const double* xv, const double* yv) {
 #pragma unroll
-        for (int i = 0; i < kB; ++i) {
-          xb[i] = Xs[8 * i];
-          yb[i] = Ys[8 * i];
-        }
+        for (int i = 0; i < kB; ++i) acc = fma(xv[i], yv[i], acc);
+      };
+      if (nfull > 0) rd(xa, ya, 0);
+      for (int j = 0; j < nfull; j += 2 * kB) {  // uniform
+        // (scheduling barriers keep each batch's reads ahead of the other
+        // batch's fmas: left alone the compiler sinks them to their use)
+        rd(xb, yb, j + kB);
+        __builtin_amdgcn_sched_barrier(0);
+        run(xa, ya);
+        __builtin_amdgcn_sched_barrier(0);
+        rd(xa, ya, j + 2 * kB < nfull ? j + 2 * kB : j);   // the last pass re-reads
+        __builtin_amdgcn_sched_barrier(0);
+        run(xb, yb);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      for (int j = 0; j < nfull; j += kB) {      // uniform
-        double2 xn[kB], yn[kB];
-        const int jn = j + kB < nfull ? j + kB : j;   // the last batch re-reads its own
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
-          xn[i] = Xs[8 * (jn + i)];
-          yn[i] = Ys[8 * (jn + i)];
-        }
-#pragma unroll
-        for (int i = 0; i < kB; ++i) step(xb[i], yb[i]);
-#pragma unroll
-        for (int i = 0; i < kB; ++i) {
-          xb[i] = xn[i];
-          yb[i] = yn[i];
-        }
-      }
-      for (int j = nfull; j < nst; ++j) step(Xs[8 * j], Ys[8 * j]);
+      for (int j = nfull; j < nst; ++j) acc = fma(Xs[8 * j], Ys[8 * j], acc);
     }
 #if VSIG_REFINE_TRACE
-    if (tid == 0) g_rtz[tb == 0 ? 2 : 3] = wall_clock64() + 0 * (unsigned long long)__double_as_longlong(d0);
-    if (tid == 0 && tb == 0) g_rtz[7] = clock64() + 0 * (unsigned long long)__double_as_longlong(d0);
+    if (tid == 0) g_rtz[tb == 0 ? 2 : 3] = wall_clock64() + 0 * (unsigned long long)__double_as_longlong(acc);
+    if (tid == 0 && tb == 0) g_rtz[7] = clock64() + 0 * (unsigned long long)__double_as_longlong(acc);
 #endif
   }
-  if (tid < 8) {                                  // lanes 0..7 of wave 0
-    auto tree = [](double u) {
-      u = u + __shfl_xor(u, 2, 8);
-      u = u + __shfl_xor(u, 4, 8);
-      return u + __shfl_xor(u, 1, 8);
-    };
-    d0 = tree(d0);
-    d1 = tree(d1);
-    d2 = tree(d2);
-    d3 = tree(d3);
+  if (tid < 32) {                                 // lanes 0..31 of wave 0
+    acc = acc + __shfl_xor(acc, 2, 8);
+    acc = acc + __shfl_xor(acc, 4, 8);
+    acc = acc + __shfl_xor(acc, 1, 8);            // lane 8 comp: d_comp
+    double d0 = acc;
+    const double d1 = __shfl(acc, 8), d2s = __shfl(acc, 16), d3s = __shfl(acc, 24);
     if (tid == 0) {
+      double d1t = d1, d2 = d2s, d3 = d3s;
       for (long long t = n8; t < w; ++t) {
         const double2 x = ld2<T>(a, ax + c0 + t), y = ld2<T>(v, c0 + t);
         const double yi = -y.y;
         d0 = fma(x.x, y.x, d0);
-        d1 = fma(x.y, yi, d1);
+        d1t = fma(x.y, yi, d1t);
         d2 = fma(x.x, yi, d2);
         d3 = fma(y.x, x.y, d3);
       }
-      double r = d0 - d1;
+      double r = d0 - d1t;
       const double m = d2 + d3;
       r = fma(m, 0.0, r);
       re = r;
@@ -708,6 +743,10 @@ __device__ __forceinline__ bool numpy_pass(
     unsigned long long hi_p1, long long vb, long long nb, long long& nact, long long it0 = -1,
     long long item0 = 0) {
   const int tid = threadIdx.x;
+  __shared__ double tiles[4 * kTile + 4 * kTilePad];
+  __shared__ int slast;
+  __shared__ double wm[kNpThreads / 64];
+  __shared__ long long wi[kNpThreads / 64];
   RT(t0);
 #if VSIG_REFINE_TRACE
   if (tid == 0) atomicMin(&g_rt_first[1], t0);
@@ -724,7 +763,7 @@ __device__ __forceinline__ bool numpy_pass(
     if (cnt == 0) return false;                    // uniform: no block counts itself
     n = (long long)cnt * g.per_item;
     if (g.cap > 0 && n > g.cap) {                  // opt-in limit: record left fp32
-      if (vb == 0 && tid == 0) keys->status = 1;
+      if (vb == 0 && tid == 0) st_agent(&keys->status, 1ull);
       return false;
     }
     lo = (long long)~lo_inv;
@@ -744,12 +783,14 @@ __device__ __forceinline__ bool numpy_pass(
   const long long ntask = dense ? ngroups + nleft + nright : n;
   // blocks past the task count take no part (the last-block hand-off counts
   // only the nact blocks that have work)
-  nact = ntask < nb ? ntask : nb;
-  if (vb >= nact) return false;
-  __shared__ double tiles[4 * kTile];
-  __shared__ int slast;
-  __shared__ double wm[kNpThreads / 64];
-  __shared__ long long wi[kNpThreads / 64];
+  // with many more blocks than tasks every S-th block (S <= 4) takes one, so
+  // that the latency-bound chains of two tasks do not share a CU
+  long long S = nb >= 2 * ntask ? nb / ntask : 1;
+  S = S < 4 ? S : 4;
+  const long long nbe = nb / S;
+  nact = ntask < nbe ? ntask : nbe;
+  if (vb % S != 0 || vb / S >= nact) return false;
+  const long long vbi = vb / S;
   RT(t1);
   double bm = -1.0;
   long long bi = 0x7fffffffffffffffLL;
@@ -759,7 +800,7 @@ __device__ __forceinline__ bool numpy_pass(
     if (cv) cv[o] = make_double2(re, im);
     if (vals) vals[o - lo] = av;
   };
-  for (long long t = vb; t < ntask; t += nb) {     // uniform per block
+  for (long long t = vbi; t < ntask; t += nbe) {   // uniform per block
     if (dense && t < ngroups) {
       const long long ob = ilo + 256 * t + 64 * (tid >> 6);
       double re, im;
@@ -797,10 +838,10 @@ __device__ __forceinline__ bool numpy_pass(
   __syncthreads();
   if (tid == 0) {
     for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
-    slots[vb] = RefineSlot{bm, bi};
-    __threadfence();
+    st_agent(&slots[vbi].m, bm);
+    st_agent(&slots[vbi].i, bi);
+    stores_done();
     slast = atomicAdd(&keys->done, 1ull) == (unsigned long long)nact - 1;
-    if (slast) __threadfence();
   }
   __syncthreads();
   if (!slast) return false;
@@ -827,10 +868,10 @@ __device__ __forceinline__ bool numpy_pass(
   if (tid == 0) {
     for (int q = 1; q < kNpThreads / 64; ++q) betterd(bm, bi, wm[q], wi[q]);
     if (rec && bm >= 0.0) {
-      rec->max2 = bm;                              // numpy's |c| at its argmax
-      rec->idx = bi;
+      st_agent(&rec->max2, bm);                    // numpy's |c| at its argmax
+      st_agent(&rec->idx, bi);
     }
-    keys->done = 0;
+    st_agent(&keys->done, 0ull);
 #if VSIG_REFINE_TRACE
     const unsigned long long tf = g_rt_first[1], t4 = wall_clock64();
     g_rt_first[1] = ~0ull;
@@ -898,15 +939,15 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
   __syncthreads();
   const long long tk = stk;
   if (tk < g1) {
-    if (finalize_select_block(f, (int)tk, g1) && tid == 0) {
-      __threadfence();                             // keys + items, then the flag
-      __hip_atomic_store(&fc->flag, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    if (finalize_select_block(f, (int)tk, g1) && tid == 0)
+      st_agent(&fc->flag, 1ull);                   // keys + items completed before
     return;
   }
   const long long vb = tk - g1;
-  // the item of this block's first task in the sparse form, read with the keys
-  const long long it0 = vb / f.g.per_item;
+  // the item of this block's first task in the sparse form (a handful of
+  // candidate outputs: every 4th numpy block takes one, numpy_pass), read
+  // with the keys
+  const long long it0 = (vb / 4) / f.g.per_item;
   if (tid == 0) {
     // the first 64 numpy blocks poll every ~1300 clocks (the usual handful of
     // candidates), the rest every ~8000 (they matter only for a dense pass);
@@ -915,13 +956,10 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
       if (vb < 64) __builtin_amdgcn_s_sleep(20);
       else __builtin_amdgcn_s_sleep(127);
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    skeys[0] = __hip_atomic_load(&f.keys->count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    skeys[1] = __hip_atomic_load(&f.keys->lo_inv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    skeys[2] = __hip_atomic_load(&f.keys->hi_p1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sitem0 = it0 < f.maxitems
-                 ? __hip_atomic_load(&f.items[it0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                 : 0;
+    skeys[0] = ld_agent(&f.keys->count);
+    skeys[1] = ld_agent(&f.keys->lo_inv);
+    skeys[2] = ld_agent(&f.keys->hi_p1);
+    sitem0 = it0 < f.maxitems ? ld_agent(f.items + it0) : 0;
     atomicAdd(&fc->seen, 1ull);
   }
   __syncthreads();
