@@ -312,6 +312,20 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
     }
 #if VSIG_REFINE_TRACE
     if (tid == 0) g_rtz[5] = wall_clock64();
+    {   // the same loads again (lines and translations now warm): latency of a warm round trip
+      double z = 0.0;
+      for (long long i0 = lo + tid; i0 < hi; i0 += 256 * kL) {
+        double p[kL];
+#pragma unroll
+        for (int q = 0; q < kL; ++q) {
+          const long long i = i0 + 256LL * q;
+          p[q] = i < hi ? *reinterpret_cast<const volatile double*>(&f.parts[i].sum_abs) : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < kL; ++q) z += p[q];
+      }
+      if (tid == 0) g_rtz[6] = wall_clock64() + 0 * (unsigned long long)__double_as_longlong(z);
+    }
 #endif
     __shared__ PeakPartial r0[1];
     block_partial<256>(m, mi, s1, s2, r0);
@@ -428,9 +442,10 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
 #if VSIG_REFINE_TRACE
     const unsigned long long tf = g_rt_first[0];
     g_rt_first[0] = ~0ull;
-    printf("RT fin g1=%d nc=%d items=%llu per_item=%lld | first->t0 %.2f loads %.2f hand %.2f "
+    printf("RT fin g1=%d nc=%d items=%llu per_item=%lld | first->t0 %.2f loads %.2f (again %.2f) hand %.2f "
            "lvl2 %.2f clist %.2f select %.2f total %.2f us\n",
-           g1, nc, scount, f.g.per_item, (rt0 - tf) * 0.01, (g_rtz[5] - rt0) * 0.01, (rt2 - rt1) * 0.01,
+           g1, nc, scount, f.g.per_item, (rt0 - tf) * 0.01, (g_rtz[5] - rt0) * 0.01,
+           ((long long)g_rtz[6] - (long long)g_rtz[5]) * 0.01, (rt2 - rt1) * 0.01,
            (rt3 - rt2) * 0.01, (rt4 - rt3) * 0.01, (rt5 - rt4) * 0.01, (rt5 - tf) * 0.01);
 #endif
   }
