@@ -436,9 +436,12 @@ def _warn_unrefined(ctx):
 def cross_correlate_signals(signal1, signal2, mode="full"):
     """utils.py:1258-1295: ``np.correlate(signal2, signal1, mode)`` and the lag
     axis.  numpy inputs -> complex128 numpy: the FFT pass runs in complex64, the
-    outputs within the refine band of the peak are recomputed by direct sums
-    in double precision (find_correlation_peak over the result then agrees
-    with numpy's argmax); elsewhere complex64 accuracy."""
+    outputs within the refine band of the peak -- however many (a tone puts
+    every full-overlap output there) -- are recomputed in numpy's own
+    operation order, so find_correlation_peak over the result gives numpy's
+    argmax and |c| to the bit; elsewhere complex64 accuracy.  A 'refine_cap'
+    option > 0 (an explicit opt-in; default none) leaves a larger band at
+    fp32 accuracy with a RuntimeWarning (refine_status)."""
     _check_mode(mode)
     ctx = _lib.get_context()
     dev = _is_dev(signal1) or _is_dev(signal2)
