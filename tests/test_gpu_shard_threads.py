@@ -50,7 +50,7 @@ def _run_ranks(world, body):
     return res
 
 
-@pytest.mark.parametrize("world,decim", [(2, 4), (3, 4), (2, 1)])
+@pytest.mark.parametrize("world,decim", [(2, 4), (3, 4), (2, 1), (4, 4), (8, 4)])
 def test_stream_chain_hip_ranks(gpu, world, decim):
     from vector_amd.shard import (ChainConfig, HipBackend, Loopback, NativeTransport,
                                   StreamChain)
@@ -108,7 +108,7 @@ def test_stream_chain_hip_ranks(gpu, world, decim):
             assert pk[2] == pytest.approx(pw[2], rel=1e-5)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_pfb_chain_hip_ranks(gpu, world):
     from vector_amd.shard import HipPfbBackend, Loopback, NativeTransport, PfbChain
     C, P = 64, 16

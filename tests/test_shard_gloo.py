@@ -138,7 +138,8 @@ def _run(world, n_local, decim, nfft, ntaps, L, freq_shift=0.0, k0s=None, read_e
 
 @pytest.mark.parametrize("world,decim,L,freq_shift", [
     (2, 2, 100, 0.0), (3, 2, 100, 0.0), (1, 2, 100, 0.0), (2, 1, 100, 0.0), (3, 1, 300, 0.0),
-    (2, 1, 450, 0.0), (3, 2, 100, FS), (2, 2, 100, FS)])
+    (2, 1, 450, 0.0), (3, 2, 100, FS), (2, 2, 100, FS),
+    (4, 4, 100, 0.0), (8, 4, 100, 0.0), (8, 1, 100, 0.0)])   # the driver's N = 4 / 8 shapes
 def test_sharded_chain_matches_single_stream(world, decim, L, freq_shift):
     """decim 1: the left halo's split at ntaps-1 outputs; long templates (L up
     to 450) widen the right halo.  freq_shift: the mixer before the FIR, phase
