@@ -54,9 +54,9 @@
 // an array (launch_refine_values: the exact confidence statistics of
 // find_correlation_peak on a flat |c|, see reduce.hip np_stats).
 // All sizes on the device (no host synchronisation).  Cross-block hand-offs
-// (last block to finish, and refine_fused's published keys) use one
-// agent-scope fence per block and agent-scope atomic loads of what other
-// blocks wrote.
+// (last block to finish, and refine_fused's published keys) write with
+// agent-scope atomic stores completed before the counter / flag, and read
+// with agent-scope atomic loads: no L2 write-back fences (stores_done).
 #include "os_common.hpp"
 
 namespace vsig {
