@@ -114,7 +114,10 @@ int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
 /* Outcome of the context's last refine pass (synchronises the stream):
  * status 0 refined, 1 skipped (more candidate outputs than a refine_cap set
- * > 0), 2 no pass ran (refine off, or no correlation yet); candidates =
+ * > 0), 2 no pass ran (refine off, or no correlation yet), 3 the one-launch
+ * refine's watchdog fired (a block waited > 2 s for the published keys: a
+ * device fault, never seen in operation; the record may be the fp32 one);
+ * candidates =
  * candidate items (thread columns of the M = 16384 / 32768 correlators, waves
  * of the M = 4096 / 8192 ones, 64-output chunks of a stored array). */
 int vsig_refine_status(vsig_ctx* ctx, int32_t* status, int64_t* candidates);

@@ -932,6 +932,12 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
 // (no co-residency assumption, other kernels may share the CUs).  The four
 // counters (zero between launches) are reset by the last numpy block once
 // every numpy block has read the keys.
+// Watchdog on refine_fused's two waits (s_memrealtime, 100 MHz): the waits
+// end by construction (a numpy block waits only for blocks that started
+// before it, which never wait), so this bound only turns a fault -- or a
+// future edit that breaks the protocol -- into status 3 instead of a hung GPU.
+constexpr unsigned long long kWatchdogTicks = 200000000ull;   // 2 s
+
 struct FusedCounters {
   unsigned long long done_a;   // FinalizeSelect::done (first-level blocks finished)
   unsigned long long ticket;   // blocks started
@@ -967,11 +973,18 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
     // the first 64 numpy blocks poll every ~1300 clocks (the usual handful of
     // candidates), the rest every ~8000 (they matter only for a dense pass);
     // one 64-byte line holds the flag alone
+    const unsigned long long w0 = wall_clock64();
+    bool timed_out = false;
     while (__hip_atomic_load(&fc->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
+      if (wall_clock64() - w0 > kWatchdogTicks) {
+        timed_out = true;
+        break;
+      }
       if (vb < 64) __builtin_amdgcn_s_sleep(20);
       else __builtin_amdgcn_s_sleep(127);
     }
-    skeys[0] = ld_agent(&f.keys->count);
+    if (timed_out) st_agent(&f.keys->status, 3ull);
+    skeys[0] = timed_out ? 0 : ld_agent(&f.keys->count);
     skeys[1] = ld_agent(&f.keys->lo_inv);
     skeys[2] = ld_agent(&f.keys->hi_p1);
     sitem0 = it0 < f.maxitems ? ld_agent(f.items + it0) : 0;
@@ -983,8 +996,14 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
                                   skeys[0], skeys[1], skeys[2], vb, kNpGrid, nact,
                                   (unsigned long long)it0 < skeys[0] ? it0 : -1, sitem0);
   if (tid == 0 && (last || (nact == 0 && vb == 0))) {
-    while (__hip_atomic_load(&fc->seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)kNpGrid)
+    const unsigned long long w0 = wall_clock64();
+    while (__hip_atomic_load(&fc->seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)kNpGrid) {
+      if (wall_clock64() - w0 > kWatchdogTicks) {
+        st_agent(&f.keys->status, 3ull);
+        break;
+      }
       __builtin_amdgcn_s_sleep(20);
+    }
     __hip_atomic_store(&fc->seen, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&fc->flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&fc->ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

@@ -582,7 +582,7 @@ int vsig_refine_status(vsig_ctx* c, int32_t* status, int64_t* candidates) {
   unsigned long long keys[4];     // refine.hip RefineKeys: count, lo_inv, hi_p1, status
   HIPCHK(c, hipMemcpyAsync(keys, c->rscratch, sizeof(keys), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  *status = keys[3] ? 1 : 0;
+  *status = keys[3] == 3 ? 3 : keys[3] ? 1 : 0;
   *candidates = (int64_t)keys[0];
   return VSIG_OK;
 }

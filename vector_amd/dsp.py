@@ -419,7 +419,8 @@ def _correlate_dev(a, v, mode, want_array, ctx, out128=False):
 def refine_status(ctx=None):
     """(status, candidates) of the last correlation's argmax refine:
     0 refined, 1 skipped (more candidate outputs than a 'refine_cap' option
-    set > 0; the default is no limit), 2 no refine pass ran."""
+    set > 0; the default is no limit), 2 no refine pass ran, 3 the refine's
+    watchdog fired (vsig.h vsig_refine_status)."""
     ctx = ctx or _lib.get_context()
     st, nc = C.c_int32(), C.c_int64()
     ctx.check(ctx.lib.vsig_refine_status(ctx.h, C.byref(st), C.byref(nc)), "refine_status")
@@ -431,6 +432,9 @@ def _warn_unrefined(ctx):
     if st == 1:
         warnings.warn(f"correlation argmax left at fp32 accuracy: the {nc} candidate items within "
                       f"the refine band exceed the 'refine_cap' option", RuntimeWarning, stacklevel=3)
+    elif st == 3:
+        warnings.warn("correlation argmax refine: watchdog fired (device fault), the peak may be "
+                      "the fp32 one", RuntimeWarning, stacklevel=3)
 
 
 def cross_correlate_signals(signal1, signal2, mode="full"):
