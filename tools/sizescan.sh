@@ -1,3 +1,5 @@
+# Size scan of the chain stages (c2 at 2^27..2^29, c5 at 2^29..2^31 samples): one bench line
+# per size into gpurun_out/r04_scan_<cfg>_<log2 n>.json (round 4, FIR / PSD / correlator scaling).
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 for s in 27 28 29; do
