@@ -54,4 +54,9 @@ for v in range(28, 34):
     name = f"read4to1_u{U}" + ("_ntl" if v & 1 else "")
     ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
     res[name] = (round(ms, 4), round(10 * n / ms / 1e6, 1))   # 8 B read + 2 B written per sample
+for v in range(40, 46):       # the same 4:1 pattern with LDS-DMA loads (global_load_lds_dwordx4)
+    U = (2, 4, 8)[(v - 40) // 2]
+    name = f"read4to1_glds_u{U}" + ("_nt" if v & 1 else "")
+    ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
+    res[name] = (round(ms, 4), round(10 * n / ms / 1e6, 1))
 print(json.dumps(res))

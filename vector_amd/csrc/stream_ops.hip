@@ -278,8 +278,54 @@ __global__ __launch_bounds__(256) void reduce4_probe(const f4v* __restrict__ x, 
   }
 }
 
+// The same 4:1 pattern with the loads as LDS-DMA (global_load_lds_dwordx4:
+// each wave-instruction lands 1 KB in the wave's LDS slice, no VGPR
+// destination), read back with ds_read_b128 once the wave's DMAs are done.
+// AUX 2: the non-temporal policy.
+template <int U, int AUX>
+__global__ __launch_bounds__(256) void reduce4_glds_probe(const f4v* __restrict__ x, long long n4,
+                                                          f2v* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) f4v slab[4][U][64];
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const long long base = ((long long)blockIdx.x * 256) * U + 64LL * U * w;   // the wave's rows
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + 64LL * u + l;
+    const f4v* src = x + (i < n4 ? i : n4 - 1);
+#if defined(__HIP_DEVICE_COMPILE__)   // a device builtin: the host pass only needs the stub
+    __builtin_amdgcn_global_load_lds(src, &slab[w][u][0], 16, 0, AUX);
+#else
+    (void)src;
+#endif
+  }
+  __builtin_amdgcn_s_waitcnt(0x3f70);   // vmcnt(0): the wave's DMAs have landed (gfx9 encoding)
+  f4v v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) v[u] = slab[w][u][l];
+#pragma unroll
+  for (int u = 0; u < U; u += 2) {
+    const long long i = ((long long)blockIdx.x * 256) * (U / 2) + 64LL * (U / 2) * w + 64LL * (u / 2) + l;
+    const f4v s = v[u] + v[u + 1];
+    if (i < n4 / 2) y[i] = f2v{s.x + s.z, s.y + s.w};
+  }
+}
+
 hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
                              hipStream_t st) {
+  if (variant >= 40) {      // LDS-DMA read-mostly probes: 40 + (U index)*2 + NT, U = 2, 4, 8
+    const int ui = (variant - 40) / 2, nt = variant & 1;
+    const long long n4 = n / 2;
+    const int U = ui == 0 ? 2 : ui == 1 ? 4 : 8;
+    const dim3 g((unsigned)((n4 + 256LL * U - 1) / (256LL * U))), b(256);
+    const f4v* x4 = reinterpret_cast<const f4v*>(x);
+    f2v* y2 = reinterpret_cast<f2v*>(y);
+#define VSIG_RG_(UU)                                                                       \
+    if (nt) hipLaunchKernelGGL((reduce4_glds_probe<UU, 2>), g, b, 0, st, x4, n4, y2);        \
+    else hipLaunchKernelGGL((reduce4_glds_probe<UU, 0>), g, b, 0, st, x4, n4, y2);
+    if (U == 2) { VSIG_RG_(2) } else if (U == 4) { VSIG_RG_(4) } else { VSIG_RG_(8) }
+#undef VSIG_RG_
+    return hipGetLastError();
+  }
   if (variant >= 28) {      // read-mostly probes: 28 + (U index)*2 + NTL, U = 2, 4, 8
     const int ui = (variant - 28) / 2, ntl = variant & 1;
     const long long n4 = n / 2;
