@@ -114,6 +114,7 @@ struct RefineSlot { double m; long long i; };   // one per numpy-pass block
 
 constexpr int kNpThreads = 256;
 constexpr int kNpGrid = 512;                   // 2 blocks per CU (64 KB of LDS each)
+constexpr int kNpFast = 64;                    // refine_fused: ticketed numpy blocks
 constexpr int kTile = 2048;                    // 4 x 16 KB of LDS
 constexpr int kTilePad = 8;                    // doubles: 64 B = 16 LDS banks
 constexpr long long kBlasThreadMin = 10000;    // zdotu_k: threads only above this n
@@ -798,14 +799,10 @@ __device__ __forceinline__ bool numpy_pass(
   const long long ntask = dense ? ngroups + nleft + nright : n;
   // blocks past the task count take no part (the last-block hand-off counts
   // only the nact blocks that have work)
-  // with many more blocks than tasks every S-th block (S <= 4) takes one, so
-  // that the latency-bound chains of two tasks do not share a CU
-  long long S = nb >= 2 * ntask ? nb / ntask : 1;
-  S = S < 4 ? S : 4;
-  const long long nbe = nb / S;
+  const long long nbe = nb;
   nact = ntask < nbe ? ntask : nbe;
-  if (vb % S != 0 || vb / S >= nact) return false;
-  const long long vbi = vb / S;
+  if (vb >= nact) return false;
+  const long long vbi = vb;
   RT(t1);
   double bm = -1.0;
   long long bi = 0x7fffffffffffffffLL;
@@ -924,18 +921,20 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
 }
 
 // The fused correlator's whole refine in one launch: g1 finalize / select
-// blocks, then kNpGrid numpy blocks.  Blocks take tickets in the order they
-// start; tickets < g1 run finalize_select_block and exit (the last one
-// publishes the keys with a flag), tickets >= g1 wait for the flag and run the
-// numpy pass.  A numpy block only ever waits for blocks that started before
-// it and never wait themselves, so the launch finishes whatever the residency
-// (no co-residency assumption, other kernels may share the CUs).  The four
-// counters (zero between launches) are reset by the last numpy block once
-// every numpy block has read the keys.
+// blocks, then kNpGrid numpy blocks.  The first g1 + kNpFast blocks (by
+// index) take tickets in the order they start; tickets < g1 run
+// finalize_select_block and exit (the last one publishes the keys with a
+// flag), tickets >= g1 are the numpy blocks a sparse pass uses; the blocks
+// after them (dense-pass helpers) keep their index.  Every numpy block waits
+// for the flag: a ticketed one only for blocks that started before it and
+// never wait, whatever the residency; a helper relies on the dispatcher
+// starting workgroups in index order (every ticketed block is then running or
+// done when a helper starts), as CDNA's does.  The four counters (zero
+// between launches) are reset by the last numpy block once every numpy block
+// has read the keys.
 // Watchdog on refine_fused's two waits (s_memrealtime, 100 MHz): the waits
-// end by construction (a numpy block waits only for blocks that started
-// before it, which never wait), so this bound only turns a fault -- or a
-// future edit that breaks the protocol -- into status 3 instead of a hung GPU.
+// end by the argument above, so this bound only turns a fault -- or a
+// dispatcher that broke index order -- into status 3 instead of a hung GPU.
 constexpr unsigned long long kWatchdogTicks = 200000000ull;   // 2 s
 
 struct FusedCounters {
@@ -956,7 +955,14 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
   const int tid = threadIdx.x;
   __shared__ long long stk, sitem0;
   __shared__ unsigned long long skeys[3];
-  if (tid == 0) stk = (long long)atomicAdd(&fc->ticket, 1ull);
+  // tickets for the first g1 + kNpFast blocks only (the finalize roles and
+  // the numpy blocks a sparse pass uses); the rest are helpers of a dense
+  // pass that keep their block index (one atomic per block on one address
+  // costs ~15 ns of serialisation: 683 tickets at config 5 were ~7 us of the
+  // finalize's start)
+  const int nticket = g1 + kNpFast;
+  if (tid == 0) stk = (int)blockIdx.x < nticket ? (long long)atomicAdd(&fc->ticket, 1ull)
+                                                 : (long long)blockIdx.x;
   __syncthreads();
   const long long tk = stk;
   if (tk < g1) {
@@ -965,14 +971,12 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
     return;
   }
   const long long vb = tk - g1;
-  // the item of this block's first task in the sparse form (a handful of
-  // candidate outputs: every 4th numpy block takes one, numpy_pass), read
-  // with the keys
-  const long long it0 = (vb / 4) / f.g.per_item;
+  // the item of this block's first task in the sparse form, read with the keys
+  const long long it0 = vb / f.g.per_item;
   if (tid == 0) {
-    // the first 64 numpy blocks poll every ~1300 clocks (the usual handful of
-    // candidates), the rest every ~8000 (they matter only for a dense pass);
-    // one 64-byte line holds the flag alone
+    // the kNpFast ticketed numpy blocks poll every ~1300 clocks (the usual
+    // handful of candidates), the helpers every ~8000 (they matter only for
+    // a dense pass); one 64-byte line holds the flag alone
     const unsigned long long w0 = wall_clock64();
     bool timed_out = false;
     while (__hip_atomic_load(&fc->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
@@ -980,7 +984,7 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
         timed_out = true;
         break;
       }
-      if (vb < 64) __builtin_amdgcn_s_sleep(20);
+      if (vb < kNpFast) __builtin_amdgcn_s_sleep(20);
       else __builtin_amdgcn_s_sleep(127);
     }
     if (timed_out) st_agent(&f.keys->status, 3ull);
