@@ -267,10 +267,55 @@ def _launcher_selftest(args, world, rank, local):
         time.sleep(120)
     t = torch.tensor([rank + 1.0])
     dist.all_reduce(t)
+    # the per-rank diagnostics' gather and summary, on made-up numbers (rank r's
+    # stages r + 1 ms, its right-halo wait 0.1 r ms; the last rank the slowest)
+    row = rank_row(1e-3 * (10 + rank) * 5, 5, {"fir": 1.0 + rank, "psd": 0.5, "xcorr": 2.0},
+                   {"right_halo": 0.1 * rank, "gather": 0.01})
+    ranks = summarize_ranks(gather_rank_rows(row, world, torch.device("cpu")))
     if rank == 0:
         print(json.dumps({"metric": METRIC, "n_gpus": world, "rccl_world": dist.get_world_size(),
-                          "sum_ranks": float(t.item())}), flush=True)
+                          "sum_ranks": float(t.item()), "ranks": ranks}), flush=True)
     dist.destroy_process_group()
+
+
+# Per-rank diagnostics at world > 1: each rank's own
+# elapsed time, its stage means (HIP events, vsig_timing) and the exposed
+# waits of its exchanges (StreamChain.enable_wait_timing), all-gathered.
+RANK_FIELDS = ("ms_per_step", "fir", "psd", "xcorr", "refine", "left_halo_wait",
+               "right_halo_wait", "gather_wait")
+
+
+def rank_row(elapsed, steps, stages, waits):
+    """One rank's diagnostics in ms (per step; a stage or wait it lacks is 0)."""
+    row = {"ms_per_step": elapsed / steps * 1e3}
+    for k in ("fir", "psd", "xcorr", "refine"):
+        row[k] = float(stages.get(k, 0.0))
+    for k in ("left_halo", "right_halo", "gather"):
+        row[k + "_wait"] = float(waits.get(k, 0.0))
+    return row
+
+
+def gather_rank_rows(row, world, dev):
+    """All ranks' rows on every rank (a float64 all-gather: RCCL on the GPU,
+    gloo on the CPU)."""
+    mine = torch.tensor([row[k] for k in RANK_FIELDS], dtype=torch.float64, device=dev)
+    out = torch.empty(world * len(RANK_FIELDS), dtype=torch.float64, device=dev)
+    dist.all_gather_into_tensor(out, mine)
+    vals = out.cpu().view(world, len(RANK_FIELDS)).tolist()
+    return [dict(zip(RANK_FIELDS, v)) for v in vals]
+
+
+def summarize_ranks(rows):
+    """min / max (and the rank holding the max) of every field over the ranks,
+    the rank that set ms_per_step (the max over ranks), and the rows."""
+    out = {"world": len(rows)}
+    for k in RANK_FIELDS:
+        v = [r[k] for r in rows]
+        i = int(np.argmax(v))
+        out[k] = {"min": round(min(v), 4), "max": round(v[i], 4), "max_rank": i}
+    out["pace_rank"] = out["ms_per_step"]["max_rank"]
+    out["per_rank"] = [{k: round(r[k], 4) for k in RANK_FIELDS} for r in rows]
+    return out
 
 
 def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
@@ -311,6 +356,7 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
     lib, h = be.ctx.lib, be.ctx.h
     lib.vsig_timing_reset(h)
     lib.vsig_timing_enable(h, 0 if args.no_kernel_timing else 1)
+    chain.enable_wait_timing(world > 1 and not args.no_kernel_timing)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
@@ -321,10 +367,6 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
     barrier()
     lib.vsig_timing_enable(h, 0)
     elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
 
     # per-kernel durations from HIP events on the launch stream
     import ctypes as C
@@ -334,6 +376,15 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
         lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
         if cnt.value:
             stages[name] = tot.value / cnt.value
+    ranks = None
+    if world > 1:
+        # every rank's own clock, stage means and exposed waits, gathered so the
+        # line says which rank and which exchange set the pace
+        waits = chain.wait_ms(steps)
+        chain.enable_wait_timing(False)
+        rows = gather_rank_rows(rank_row(elapsed, steps, stages, waits), world, dev)
+        ranks = summarize_ranks(rows)
+        elapsed = max(r["ms_per_step"] for r in rows) * steps * 1e-3
     ny = n // decim
     bytes_per_launch = {"fir": 8 * n + 8 * ny, "psd": 8 * ny + 4 * ny,
                         "xcorr": 8 * (ny + chain.yhalo)}
@@ -412,7 +463,7 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
                            "hbm_frac": round(chain_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "bytes_basis": f"{chain_bytes / n:.2f} B/input sample"}
     return {"elapsed": elapsed, "stages": stages, "stage_roof": stage_roof, "roof": roof,
-            "check": check, "taps": taps, "tmpl": tmpl}
+            "check": check, "taps": taps, "tmpl": tmpl, "ranks": ranks}
 
 
 def main():
@@ -545,6 +596,7 @@ def main():
         "stages_roofline_c2": stages_c2,
         "check": check,
         "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
+        "ranks": leg["ranks"],
     }
     print(json.dumps(out), flush=True)
     if world > 1:

@@ -45,6 +45,8 @@ extern "C" {
 #define VSIG_E_NOMEM -3       /* device allocation failed */
 #define VSIG_E_UNSUPPORTED -4 /* size outside what the kernels implement */
 #define VSIG_E_NODEVICE -5    /* no HIP device */
+#define VSIG_E_REFINE -6      /* the exact-argmax refine faulted (watchdog, status 3):
+                                 the peak record must not be used */
 
 #define VSIG_MODE_VALID 0
 #define VSIG_MODE_FULL 1
@@ -109,14 +111,20 @@ int vsig_synchronize(vsig_ctx* ctx);
  *                     1 ms per 2^20 outputs x 4096 terms); > 0 (>= 4096): an
  *                     explicit limit on candidate outputs -- beyond it the
  *                     record is left as the fp32 pass produced it and
- *                     vsig_refine_status reports status 1. */
+ *                     vsig_refine_status reports status 1;
+ *   "refine_watchdog_us" bound on the one-launch refine's two waits (default
+ *                     2000000; a test hook: tiny values force a fire, status 3). */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
 /* Outcome of the context's last refine pass (synchronises the stream):
  * status 0 refined, 1 skipped (more candidate outputs than a refine_cap set
  * > 0), 2 no pass ran (refine off, or no correlation yet), 3 the one-launch
- * refine's watchdog fired (a block waited > 2 s for the published keys: a
- * device fault, never seen in operation; the record may be the fp32 one);
+ * refine's watchdog fired in some pass since the last call (a block waited
+ * longer than the "refine_watchdog_us" option, default 2 s, for the published
+ * keys: a device fault, never seen in operation).  Status 3 is an error: the
+ * record's index is poisoned (-1) and its values must not be used; this call
+ * reports it once and clears the refine's counters so the context's next
+ * correlation starts clean (vsig_chain_result returns VSIG_E_REFINE instead);
  * candidates =
  * candidate items (thread columns of the M = 16384 / 32768 correlators, waves
  * of the M = 4096 / 8192 ones, 64-output chunks of a stored array). */

@@ -25,6 +25,15 @@ def test_self_launch_two_ranks(tmp_path):
     assert len(lines) == 1
     out = json.loads(lines[0])
     assert out["n_gpus"] == 2 and out["rccl_world"] == 2 and out["sum_ranks"] == 3.0
+    # the per-rank diagnostics bench.py writes at world > 1, gathered over gloo
+    rk = out["ranks"]
+    assert rk["world"] == 2 and rk["pace_rank"] == 1
+    assert rk["fir"] == {"min": 1.0, "max": 2.0, "max_rank": 1}
+    assert rk["right_halo_wait"]["max"] == 0.1 and rk["left_halo_wait"]["max"] == 0.0
+    assert rk["ms_per_step"]["max"] == 11.0
+    assert [r["ms_per_step"] for r in rk["per_rank"]] == [10.0, 11.0]
+    for k in ("fir", "psd", "xcorr", "refine", "left_halo_wait", "right_halo_wait", "gather_wait"):
+        assert set(rk[k]) == {"min", "max", "max_rank"}
     envs = [json.load(open(tmp_path / f"rank{k}.json")) for k in range(2)]
     assert [e["RANK"] for e in envs] == ["0", "1"]
     assert [e["LOCAL_RANK"] for e in envs] == ["0", "1"]

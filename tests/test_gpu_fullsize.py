@@ -9,7 +9,9 @@ the small cases do not reach.
   run on those slices with their halos, the sync lag exact.
 * C3: a 4096-sample preamble over 2**30 samples: exact lag, peak equal to the
   direct double-precision dot product (refined), sums to 1e-5.
-* C5 shape (D = 4) at 2**29 samples: decimated FIR / PSD slices and the lag.
+* C5 shape (D = 4) at 2**29 samples: decimated FIR / PSD slices and the lag;
+  and at the headline's own 2**31 samples per GPU: first / middle / last
+  slices (inputs up to index 2**31 - 1) and a preamble planted in the tail.
 Inputs are generated on the device (bench.py's generator: tones + CN(0, 1)
 noise + the planted preamble); only the checked slices come back to the host.
 """
@@ -49,14 +51,15 @@ def test_create_spectrogram_heavy_branch(gpu):
     np.testing.assert_array_equal(Sd.cpu().numpy(), S)
 
 
-def _chain(gpu, n, decim, seed):
+def _chain(gpu, n, decim, seed, k0=None):
     from vector_amd.shard import ChainConfig, HipBackend, StreamChain
     b = _bench()
     taps, pre, tmpl = b.design(255, 4096, decim)
     cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=8192, template=tmpl)
     be = HipBackend(cfg, 0)
     ch = StreamChain(cfg, be, 0, 1)
-    k0 = (n // decim // 2 + 12_345) * decim
+    if k0 is None:
+        k0 = (n // decim // 2 + 12_345) * decim
     b.generate_chunk(ch.x, 0, seed, pre, k0)
     ch.step()
     torch.cuda.synchronize()
@@ -101,6 +104,31 @@ def test_c5_shape_decimated_chain(gpu):
     assert lag == k0 // 4
     ny = n // 4
     _check_slices(ch, taps, tmpl, n, 4, [0, 8192 * 5, ny // 2, ny - 8192])
+
+
+def test_c5_headline_size_2pow31(gpu):
+    """The headline's own per-GPU size (BASELINE configs[4] on one GPU, what
+    bench.py times): 2**31 input samples (x_ext = 2**31 + 254 with the FIR
+    history, past the 32-bit index range), D = 4.  FIR outputs and PSD frames
+    of the first, a middle and the last 8192 decimated outputs against the
+    oracle on those input slices with their halos (the last slice reads input
+    samples up to 2**31 - 1, x_ext offsets up to 2**31 + 253); a preamble
+    planted in the tail of the capture (input sample ~2**31 - 2**18) is found
+    at its exact lag, with numpy's |c| (the direct double-precision dot)."""
+    n, decim = 1 << 31, 4
+    ny = n // decim
+    k0 = (ny - 60_001) * decim
+    ch, taps, tmpl, k0 = _chain(gpu, n, decim, 2031, k0=k0)
+    assert ch.x_ext.numel() > (1 << 31)
+    m, lag, s1, s2, nout = ch.global_peak()
+    assert lag == k0 // decim
+    assert nout == ny - 4096 + 1
+    seg = ch.y[lag: lag + 4096].cpu().numpy().astype(np.complex128)
+    direct = abs(np.vdot(tmpl.astype(np.complex128), seg))
+    assert m == pytest.approx(direct, rel=1e-12)
+    _check_slices(ch, taps, tmpl, n, decim, [0, ny // 2 + 8192 * 3, ny - 8192])
+    del ch
+    torch.cuda.empty_cache()
 
 
 def test_c3_sync_2pow30(gpu):

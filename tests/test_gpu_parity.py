@@ -231,10 +231,10 @@ def test_cross_correlate_small_golden(gpu):
             want = g[f"peak_{mode}"]
             assert lag == want[0]
             assert val == pytest.approx(want[1], rel=1e-5)
-            assert conf == pytest.approx(want[2], abs=1e-4)
+            assert conf == pytest.approx(want[2], rel=1e-5, abs=1e-7)
             lag2, val2, conf2 = gpu.correlate_peak(g["s1"], g["s2"], mode)
             assert lag2 == want[0] and val2 == pytest.approx(want[1], rel=1e-5)
-            assert conf2 == pytest.approx(want[2], abs=1e-4)
+            assert conf2 == pytest.approx(want[2], rel=1e-5, abs=1e-7)
         else:
             with pytest.raises(IndexError):
                 gpu.find_correlation_peak(c, lags)
@@ -279,7 +279,7 @@ def test_correlate_peak_4096_preamble(gpu):
     lag, val, conf = gpu.correlate_peak(g["pre"], g["x"], "valid")
     assert lag == int(g["peak_lag"]) == int(g["k0"])
     assert val == pytest.approx(float(g["peak_val"]), rel=1e-5)
-    assert conf == pytest.approx(float(g["conf"]), abs=1e-4)
+    assert conf == pytest.approx(float(g["conf"]), rel=1e-5, abs=1e-7)
     gf = golden("xcorr_peak_full.npz")
     lag, val, conf = gpu.correlate_peak(g["pre"], g["x"], "full")
     assert lag == int(gf["peak_lag"])
@@ -304,7 +304,7 @@ def test_find_packet_location(gpu):
     got = gpu.find_packet_location_in_vector(g["loc_vector"], g["loc_packet"], g["loc_ref"])
     want = g["loc_result"]
     assert got[0] == want[0] and got[1] == want[1]
-    assert got[2] == pytest.approx(want[2], abs=1e-4)
+    assert got[2] == pytest.approx(want[2], rel=1e-5, abs=1e-7)
     got = gpu.find_packet_location_in_vector(g["loc_vector"], g["loc_packet"], g["loc_ref"],
                                              search_window=(10_000, 20_000))
     assert got[0] == g["loc_result_win"][0]
@@ -404,7 +404,7 @@ def test_correlate_peak_long_template(gpu):
     got = gpu.correlate_peak(pre, s, "valid")
     assert got[0] == want[0] == k0
     assert got[1] == pytest.approx(want[1], rel=1e-5)
-    assert got[2] == pytest.approx(want[2], rel=1e-4, abs=1e-6)
+    assert got[2] == pytest.approx(want[2], rel=1e-5, abs=1e-7)
     c, lags = gpu.cross_correlate_signals(pre, s, "valid")
     got2 = gpu.find_correlation_peak(c, lags)
     assert got2[0] == k0

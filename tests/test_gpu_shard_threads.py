@@ -146,3 +146,70 @@ def test_pfb_chain_hip_ranks(gpu, world):
     xh = xs[0][: 200 * C + len(h)].cpu().numpy()
     ref_frames = ref.pfb_channelize(xh, h, C).T
     assert np.abs(want[0][: len(ref_frames)] - ref_frames).max() <= 1e-5 * np.abs(ref_frames).max()
+
+
+def test_rank_diagnostics_world4(gpu):
+    """bench.py's per-rank line at world > 1, on the classes it drives: four
+    thread ranks (loopback transport) run three timed steps with the stage
+    timers (vsig_timing, HIP events per rank context) and the exposed-wait
+    events on (StreamChain.enable_wait_timing); bench.rank_row /
+    summarize_ranks give every field -- stage min / max over ranks, the
+    left- / right-halo and all-gather waits as measured on each rank's stream,
+    the rank that set the pace -- and every rank gets the exact lag."""
+    import ctypes as C
+    import os
+    import sys
+    import time
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    from vector_amd.shard import ChainConfig, HipBackend, Loopback, NativeTransport, StreamChain
+    world, decim, n, L = 4, 4, 1 << 19, 1024
+    N = world * n
+    taps = scipy.signal.firwin(255, 0.2).astype(np.float32)
+    pre = ref.qpsk_preamble(L * decim, seed=51)
+    tmpl = np.convolve(pre, taps)[: L * decim][::decim].astype(np.complex64)
+    x = ref.synth_iq(N, seed=52)
+    k0 = (n // decim - L // 2) * decim             # straddles ranks 0 / 1 (right halo)
+    x[k0: k0 + L * decim] += 3 * pre
+    xt = torch.from_numpy(x).cuda()
+    lb = Loopback(world)
+    steps = 3
+
+    def body(r):
+        cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=2048, template=tmpl)
+        be = HipBackend(cfg, 0)
+        ch = StreamChain(cfg, be, r, world, transport=NativeTransport(lb.transport(r)))
+        ch.x.copy_(xt[r * n:(r + 1) * n])
+        ch.step()                                    # warm-up
+        torch.cuda.current_stream().synchronize()
+        lib, h = be.ctx.lib, be.ctx.h
+        lib.vsig_timing_reset(h)
+        lib.vsig_timing_enable(h, 1)
+        ch.enable_wait_timing(True)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ch.step()
+        torch.cuda.current_stream().synchronize()
+        elapsed = time.perf_counter() - t0
+        lib.vsig_timing_enable(h, 0)
+        stages = {}
+        for k in ("fir", "psd", "xcorr", "refine"):
+            tot, cnt = C.c_double(), C.c_int64()
+            lib.vsig_timing_read(h, k.encode(), C.byref(tot), C.byref(cnt))
+            if cnt.value:
+                stages[k] = tot.value / cnt.value
+        waits = ch.wait_ms(steps)
+        return bench.rank_row(elapsed, steps, stages, waits), ch.global_peak()[1], sorted(waits)
+
+    res = _run_ranks(world, body)
+    summ = bench.summarize_ranks([r[0] for r in res])
+    print(summ)
+    assert all(r[1] == k0 // decim for r in res)
+    assert all(r[2] == ["gather", "left_halo", "right_halo"] for r in res)
+    assert summ["world"] == world and 0 <= summ["pace_rank"] < world
+    for k in bench.RANK_FIELDS:
+        assert set(summ[k]) == {"min", "max", "max_rank"}
+        assert 0.0 <= summ[k]["min"] <= summ[k]["max"] < 1e4
+    for k in ("fir", "psd", "xcorr", "refine"):
+        assert summ[k]["min"] > 0.0                  # every rank ran every stage
+    assert len(summ["per_rank"]) == world

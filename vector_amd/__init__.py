@@ -5,7 +5,7 @@ CDNA4 HIP kernels in libvsig.so (C ABI, include/vsig.h), behind the reference's
 own Python call signatures (utils.py).  No CPU fallback: without the library or
 a HIP device every call raises ``VsigUnavailable``.
 """
-from ._lib import VsigError, VsigUnavailable, get_context, load_library  # noqa: F401
+from ._lib import RefineFault, VsigError, VsigUnavailable, get_context, load_library  # noqa: F401
 from . import dsp  # noqa: F401
 from .dsp import (Correlator, FirFilter, correlate, correlate_peak,  # noqa: F401
                   cross_correlate_signals, filter, find_correlation_peak,

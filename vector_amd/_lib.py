@@ -27,6 +27,12 @@ class VsigError(RuntimeError):
     pass
 
 
+class RefineFault(VsigError):
+    """The exact-argmax refine faulted on the device (its watchdog fired,
+    vsig.h VSIG_E_REFINE / refine status 3): the peak record is invalid.
+    Raised, never warned: the lag / |c| contract is numpy's exact answer."""
+
+
 class Peak(C.Structure):
     _fields_ = [("peak", C.c_double), ("index", C.c_int64),
                 ("sum_abs", C.c_double), ("sum_abs2", C.c_double)]
@@ -216,6 +222,8 @@ class Context:
                 raise ValueError(f"{what}: {err}: {msg}")
             if rc == -4:
                 raise NotImplementedError(f"{what}: {err}: {msg}")
+            if rc == -6:
+                raise RefineFault(f"{what}: {err}: {msg}")
             raise VsigError(f"{what}: {err}: {msg}")
 
     def bind_stream(self):

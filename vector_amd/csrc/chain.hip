@@ -220,6 +220,16 @@ int vsig_chain_result(vsig_chain* ch, vsig_peak_t* peak, int64_t* nout) {
   CHK(ch, hipMemcpyAsync(rows.data(), ch->rows, sizeof(vsig_peak_t) * ch->world,
                          hipMemcpyDeviceToHost, st));
   CHK(ch, hipStreamSynchronize(st));
+  // the exact-argmax contract: a refine fault on this rank (sticky since the
+  // last check) or on any other (its gathered row's poisoned index) is an error
+  int32_t rst = 0;
+  int64_t rcand = 0;
+  int rc = vsig_refine_status(ch->ctx, &rst, &rcand);
+  if (rc) return chain_fail(ch, rc, "refine status");
+  if (rst == 3) return chain_fail(ch, VSIG_E_REFINE, "exact-argmax refine faulted on this rank");
+  for (int q = 0; q < ch->world; ++q)
+    if (rows[q].index < 0)
+      return chain_fail(ch, VSIG_E_REFINE, "exact-argmax refine faulted on rank " + std::to_string(q));
   vsig_peak_t best{-1.0, 0, 0.0, 0.0};
   bool have = false;
   double s1 = 0.0, s2 = 0.0;

@@ -106,7 +106,11 @@ struct RefineKeys {
   unsigned long long hi_p1;    // highest final output an item covers + 1 (atomic max)
   unsigned long long status;   // 1: more candidate outputs than the opt-in cap
   unsigned long long done;     // numpy-pass blocks finished (the last one reduces)
-  unsigned long long pad[3];
+  unsigned long long fault;    // sticky: a refine_fused watchdog fired.  Nothing on
+                               // the device clears it (the finalize resets status,
+                               // not this); vsig_refine_status reports status 3 and
+                               // clears it with the launch's counters.
+  unsigned long long pad[2];
 };
 static_assert(sizeof(RefineKeys) == 64, "the items follow the keys at +64 B");
 
@@ -246,6 +250,7 @@ struct FinalizeSelect {
   long long* items; long long maxitems; RefineKeys* keys;
   const unsigned* lkeys;            // optional lane keys (64 per wave partial)
   RefineGeom g;                     // item -> output spans
+  unsigned long long wd_ticks;      // refine_fused's watchdog (s_memrealtime, 100 MHz)
 };
 
 // A record another block of this launch wrote (possibly on another XCD).
@@ -263,6 +268,18 @@ __device__ __forceinline__ void st_agent(PeakPartial* o, const PeakPartial& r) {
   __hip_atomic_store(&o->idx, r.idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&o->sum_abs, r.sum_abs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&o->sum_abs2, r.sum_abs2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// A watchdog fire leaves the record unusable: index -1 (no output has it), so
+// a caller that reads the record without vsig_refine_status still cannot take
+// it for a peak (the sharded chain's gathered rows, StreamChain.global_peak).
+__device__ __forceinline__ void poison_record(PeakPartial* rec) {
+  __hip_atomic_store(&rec->idx, -1LL, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void watchdog_fired(const FinalizeSelect& f) {
+  st_agent(&f.keys->fault, 1ull);
+  stores_done();
+  poison_record(f.rec);
 }
 
 #ifndef VSIG_REFINE_TRACE
@@ -358,6 +375,8 @@ __device__ __forceinline__ bool finalize_select_block(const FinalizeSelect& f, i
       PeakPartial o = r[0];
       o.max2 = sqrt(o.max2);
       st_agent(f.rec, o);
+      stores_done();
+      if (ld_agent(&f.keys->fault)) poison_record(f.rec);   // a watchdog fired first
       const double t = o.max2 * (1.0 - f.eps);
       sthr = t > 0.0 ? t * t : 0.0;                // partials hold fp32 |c|^2
       st_agent(f.done, 0ull);
@@ -934,7 +953,9 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_numpy(
 // has read the keys.
 // Watchdog on refine_fused's two waits (s_memrealtime, 100 MHz): the waits
 // end by the argument above, so this bound only turns a fault -- or a
-// dispatcher that broke index order -- into status 3 instead of a hung GPU.
+// dispatcher that broke index order -- into status 3 (a sticky fault word and
+// a poisoned record, see RefineKeys::fault) instead of a hung GPU.  Default
+// 2 s; the context option "refine_watchdog_us" sets it (tests force fires).
 constexpr unsigned long long kWatchdogTicks = 200000000ull;   // 2 s
 
 struct FusedCounters {
@@ -980,18 +1001,19 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
     const unsigned long long w0 = wall_clock64();
     bool timed_out = false;
     while (__hip_atomic_load(&fc->flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) {
-      if (wall_clock64() - w0 > kWatchdogTicks) {
+      if (wall_clock64() - w0 > f.wd_ticks) {
         timed_out = true;
         break;
       }
       if (vb < kNpFast) __builtin_amdgcn_s_sleep(20);
       else __builtin_amdgcn_s_sleep(127);
     }
-    if (timed_out) st_agent(&f.keys->status, 3ull);
+    if (timed_out) watchdog_fired(f);
     skeys[0] = timed_out ? 0 : ld_agent(&f.keys->count);
     skeys[1] = ld_agent(&f.keys->lo_inv);
     skeys[2] = ld_agent(&f.keys->hi_p1);
     sitem0 = it0 < f.maxitems ? ld_agent(f.items + it0) : 0;
+    stores_done();                                 // a fault word before the count
     atomicAdd(&fc->seen, 1ull);
   }
   __syncthreads();
@@ -1002,12 +1024,16 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
   if (tid == 0 && (last || (nact == 0 && vb == 0))) {
     const unsigned long long w0 = wall_clock64();
     while (__hip_atomic_load(&fc->seen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned long long)kNpGrid) {
-      if (wall_clock64() - w0 > kWatchdogTicks) {
-        st_agent(&f.keys->status, 3ull);
+      if (wall_clock64() - w0 > f.wd_ticks) {
+        watchdog_fired(f);
         break;
       }
       __builtin_amdgcn_s_sleep(20);
     }
+    // every numpy block has read the keys (or the wait above fired): a fire of
+    // any of them is in the fault word by now; the record must not survive it
+    // (the reducing block may have written numpy's answer without it)
+    if (ld_agent(&f.keys->fault)) poison_record(f.rec);
     __hip_atomic_store(&fc->seen, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&fc->flag, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&fc->ticket, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1062,7 +1088,8 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
     g1 = (r.nparts + chunk - 1) / chunk;
     if (g1 < 1) g1 = 1;
     const FinalizeSelect f{r.parts, r.nparts, chunk, r.tmp, r.done, r.rec, r.eps, items,
-                           max_items(r), keys, r.lkeys, g};
+                           max_items(r), keys, r.lkeys, g,
+                           r.wd_ticks ? r.wd_ticks : kWatchdogTicks};
     const dim3 grid((unsigned)(g1 + kNpGrid));
     if (r.c128)
       hipLaunchKernelGGL(refine_fused<double2>, grid, dim3(kNpThreads), 0, st, f, (int)g1,
@@ -1074,9 +1101,10 @@ hipError_t launch_refine(const RefineArgs& r, hipStream_t st) {
                          static_cast<double2*>(r.out128));
     return hipGetLastError();
   }
-  // a stored c64 array: keys memset, select, numpy pass
+  // a stored c64 array: keys memset (up to the sticky fault word, which only
+  // vsig_refine_status clears), select, numpy pass
   if (r.cols || r.lkeys || !r.from_array) return hipErrorInvalidValue;
-  hipError_t e = hipMemsetAsync(keys, 0, sizeof(RefineKeys), st);
+  hipError_t e = hipMemsetAsync(keys, 0, offsetof(RefineKeys, fault), st);
   if (e != hipSuccess) return e;
   const long long grid = (r.nout + 255) / 256;
   hipLaunchKernelGGL(refine_select_array, dim3((unsigned)grid), dim3(256), 0, st, r.c64, r.nout,

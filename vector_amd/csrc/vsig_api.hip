@@ -17,6 +17,8 @@ struct TimingRec {
   std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
 };
 
+constexpr size_t kRefineKeysBytes = 64;   // refine.hip RefineKeys (the scratch header)
+
 struct vsig_ctx {
   int device = 0;
   hipStream_t own = nullptr;
@@ -40,6 +42,7 @@ struct vsig_ctx {
   int refine = 1;                        // exact re-rank of the correlators' peak
   int refine_eps_ppm = 1000;             // fp32 candidate band (relative, ppm of max |c|)
   long long refine_cap = 0;              // opt-in limit on candidate outputs (0: none)
+  long long refine_wd_us = 2000000;      // refine_fused watchdog (option "refine_watchdog_us")
   int blas_threads = 1;                  // numpy's OpenBLAS threads (its zdotu splits > 10000 terms)
   bool refine_ran = false;
   struct Chirp { long long M; float2* c; float2* B; };
@@ -314,8 +317,14 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
   r.eps = c->refine_eps_ppm * 1e-6;
   r.blas_threads = c->blas_threads;
   r.cap = c->refine_cap;
-  int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, vsig::refine_scratch_bytes(r));
+  r.wd_ticks = (unsigned long long)c->refine_wd_us * 100ull;   // s_memrealtime: 100 MHz
+  const size_t need = vsig::refine_scratch_bytes(r);
+  const bool fresh = need > c->rscratch_bytes;
+  int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, need);
   if (rc) return rc;
+  // a new scratch starts with zero keys (the sticky fault word is read by
+  // vsig_refine_status; the finalize resets only the per-launch words)
+  if (fresh) HIPCHK(c, hipMemsetAsync(c->rscratch, 0, kRefineKeysBytes, c->stream));
   r.scratch = c->rscratch;
   r.rec = rec;
   r.out128 = out128;
@@ -484,6 +493,7 @@ const char* vsig_errstr(int s) {
     case VSIG_E_NOMEM: return "device out of memory";
     case VSIG_E_UNSUPPORTED: return "unsupported size";
     case VSIG_E_NODEVICE: return "no HIP device";
+    case VSIG_E_REFINE: return "exact-argmax refine faulted (watchdog); peak record invalid";
     default: return "unknown status";
   }
 }
@@ -554,6 +564,9 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else if (k == "refine_cap") {
     if (value != 0 && value < 4096) return fail(c, VSIG_E_INVALID, "refine_cap must be 0 or >= 4096");
     c->refine_cap = value;
+  } else if (k == "refine_watchdog_us") {
+    if (value < 1) return fail(c, VSIG_E_INVALID, "refine_watchdog_us must be >= 1");
+    c->refine_wd_us = value;
   } else if (k == "blas_threads") {
     if (value < 1 || value > 1024) return fail(c, VSIG_E_INVALID, "blas_threads must be in [1, 1024]");
     c->blas_threads = value;
@@ -569,6 +582,7 @@ int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
   if (k == "refine") *value = c->refine;
   else if (k == "refine_eps_ppm") *value = c->refine_eps_ppm;
   else if (k == "refine_cap") *value = (int)c->refine_cap;
+  else if (k == "refine_watchdog_us") *value = (int)c->refine_wd_us;
   else if (k == "blas_threads") *value = c->blas_threads;
   else return VSIG_E_INVALID;
   return VSIG_OK;
@@ -579,11 +593,26 @@ int vsig_refine_status(vsig_ctx* c, int32_t* status, int64_t* candidates) {
   *status = 2;
   *candidates = 0;
   if (!c->refine_ran || !c->rscratch) return VSIG_OK;
-  unsigned long long keys[4];     // refine.hip RefineKeys: count, lo_inv, hi_p1, status
+  // refine.hip RefineKeys: count, lo_inv, hi_p1, status, done, fault
+  unsigned long long keys[6];
   HIPCHK(c, hipMemcpyAsync(keys, c->rscratch, sizeof(keys), hipMemcpyDeviceToHost, c->stream));
   HIPCHK(c, hipStreamSynchronize(c->stream));
-  *status = keys[3] == 3 ? 3 : keys[3] ? 1 : 0;
   *candidates = (int64_t)keys[0];
+  if (keys[5]) {
+    // a watchdog fired in some refine since the last report: status 3 once,
+    // then the fused launch's counters and the keys (fault word included) are
+    // cleared -- a fire can leave them inconsistent, and the next launch must
+    // start from zero -- and the record is not to be trusted until then
+    *status = 3;
+    HIPCHK(c, hipMemsetAsync(c->rscratch, 0, kRefineKeysBytes, c->stream));
+    if (c->partials)
+      HIPCHK(c, hipMemsetAsync(c->partials + c->npartials + vsig::kFinalizeTmp, 0,
+                               vsig::kCounterRecs * sizeof(PeakPartial), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->refine_ran = false;
+    return VSIG_OK;
+  }
+  *status = keys[3] ? 1 : 0;
   return VSIG_OK;
 }
 

@@ -170,6 +170,7 @@ struct RefineArgs {
   void* scratch;                    // refine_scratch_bytes(*this)
   PeakPartial* rec;                 // finalized record (max |c|), updated in place
   void* out128;                     // optional complex128 c to patch (final space)
+  unsigned long long wd_ticks;      // fused launch's watchdog, 100 MHz ticks (0: 2 s)
 };
 size_t refine_scratch_bytes(const RefineArgs& r);
 hipError_t launch_refine(const RefineArgs& r, hipStream_t st);

@@ -32,7 +32,7 @@ from .windows import get_window
 __all__ = ["spectrum", "filter", "fir_filter", "correlate", "correlate_peak",
            "cross_correlate_signals", "find_correlation_peak",
            "find_packet_location_in_vector", "FirFilter", "Correlator", "peak_stats",
-           "refine_status"]
+           "refine_status", "check_refine"]
 
 PEAK_BYTES = 32  # sizeof(vsig_peak_t)
 
@@ -104,23 +104,30 @@ def _confidence_np(peak, mean, std, threshold_ratio):
     return conf
 
 
-# The fused correlators sum fp32 |c| values (errors ~1e-6 of the peak); below
-# this spread (std / peak) their single-pass variance no longer resolves
-# numpy's, and the statistics are recomputed from numpy-order values
-# (vsig_correlate_stats_dev) -- a flat |c| (a tone) has a std of rounding noise.
-_FUSED_STD_FLOOR = 1e-3
+# The fused correlators sum fp32 |c| values; their single-pass variance
+# var = s2/n - mean^2 carries the sums' relative error e (~1e-7: fp32 FFT
+# outputs, fp32 per-thread sums, double beyond) amplified by (s2/n) / var.
+# Above _FUSED_VAR_FLOOR of the mean square the amplification is <= 20 and the
+# std is within ~1e-6 of numpy's (confidence to the 1e-5 bar, tests); below it
+# -- a flat |c| (a tone: std of rounding noise), or a tone under weak noise --
+# the statistics are recomputed from numpy-order values
+# (vsig_correlate_stats_dev: every output re-evaluated as np.correlate forms
+# it, then numpy's two-pass mean / std).  Rayleigh-like |c| of noise sits at
+# var / (s2/n) = 1 - pi/4 = 0.21 and keeps the fused sums.
+_FUSED_VAR_FLOOR = 0.05
 
 
 def _fused_stats(peak, s1, s2, n):
     """(mean, std, resolved) from the fused record's sums."""
     mean = s1 / n
-    var = s2 / n - mean * mean
+    ms = s2 / n
+    var = ms - mean * mean
     std = float(np.sqrt(var)) if var > 0 else 0.0
-    return mean, std, std > _FUSED_STD_FLOOR * peak
+    return mean, std, var > _FUSED_VAR_FLOOR * ms
 
 
 def _confidence(peak, s1, s2, n, threshold_ratio):
-    """The confidence from a fused record's sums (single pass; see _FUSED_STD_FLOOR)."""
+    """The confidence from a fused record's sums (single pass; see _FUSED_VAR_FLOOR)."""
     mean, std, _ = _fused_stats(peak, s1, s2, n)
     return _confidence_np(peak, mean, std, threshold_ratio)
 
@@ -420,21 +427,29 @@ def refine_status(ctx=None):
     """(status, candidates) of the last correlation's argmax refine:
     0 refined, 1 skipped (more candidate outputs than a 'refine_cap' option
     set > 0; the default is no limit), 2 no refine pass ran, 3 the refine's
-    watchdog fired (vsig.h vsig_refine_status)."""
+    watchdog fired since the last call (vsig.h vsig_refine_status; reported
+    once, the refine's counters are cleared by the call)."""
     ctx = ctx or _lib.get_context()
     st, nc = C.c_int32(), C.c_int64()
     ctx.check(ctx.lib.vsig_refine_status(ctx.h, C.byref(st), C.byref(nc)), "refine_status")
     return int(st.value), int(nc.value)
 
 
-def _warn_unrefined(ctx):
+def check_refine(ctx=None):
+    """The exact-argmax contract after a correlation: status 3 (the refine's
+    watchdog fired: a device fault) raises RefineFault; status 1 (an opt-in
+    'refine_cap' exceeded) warns -- that limit is the caller's own choice.
+    Device-tensor callers (Correlator, cross_correlate_signals on CUDA
+    tensors) run asynchronously and call this themselves when they read the
+    result (StreamChain.global_peak does)."""
+    ctx = ctx or _lib.get_context()
     st, nc = refine_status(ctx)
+    if st == 3:
+        raise _lib.RefineFault("correlation argmax refine: watchdog fired (device fault); the "
+                               "peak record is invalid (vsig_refine_status 3)")
     if st == 1:
         warnings.warn(f"correlation argmax left at fp32 accuracy: the {nc} candidate items within "
                       f"the refine band exceed the 'refine_cap' option", RuntimeWarning, stacklevel=3)
-    elif st == 3:
-        warnings.warn("correlation argmax refine: watchdog fired (device fault), the peak may be "
-                      "the fp32 one", RuntimeWarning, stacklevel=3)
 
 
 def cross_correlate_signals(signal1, signal2, mode="full"):
@@ -457,7 +472,7 @@ def cross_correlate_signals(signal1, signal2, mode="full"):
     if dev:
         return c, lags
     out = c.cpu().numpy()
-    _warn_unrefined(ctx)
+    check_refine(ctx)
     return out, lags
 
 
@@ -529,7 +544,7 @@ def correlate_peak(signal1, signal2, mode="full", threshold_ratio=0.5):
     ctx = _lib.get_context()
     _, pk, nout, (ad, vd, in128) = _correlate_dev(signal2, signal1, mode, False, ctx)
     peak, idx, s1, s2 = _read_peak(pk)
-    _warn_unrefined(ctx)
+    check_refine(ctx)
     mean, std, resolved = _fused_stats(peak, s1, s2, nout)
     if not resolved:
         # a (nearly) flat |c|: numpy's std is decided by rounding; every

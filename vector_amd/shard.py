@@ -182,6 +182,11 @@ class HipBackend:
         (max |c|, local index (int64 bits), sum |c|, sum |c|^2)."""
         self.xc(s, "valid", peak=rec)
 
+    def check_refine(self):
+        """Raise RefineFault if a refine of this rank faulted since the last
+        check (the fault word is sticky on the device; synchronises)."""
+        self.dsp.check_refine(self.ctx)
+
 
 class StreamChain:
     """One rank's part of the sharded chain (world = 1: the plain chain)."""
@@ -206,6 +211,7 @@ class StreamChain:
         self._gather = [None, None]
         self._slot = 1
         self.peak_rows = None
+        self._wt = None                   # exposed-wait events (enable_wait_timing)
 
     @property
     def x(self):
@@ -221,10 +227,45 @@ class StreamChain:
         """This step's peak record."""
         return self._recs[self._slot]
 
+    # -- per-rank diagnostics (bench.py at world > 1) --------------------------
+    def enable_wait_timing(self, on: bool = True):
+        """Bracket the step's three exposed waits with timing events on the
+        launch stream: the all-gather slot wait at the step start ('gather'),
+        the left-halo wait before the FIR's first outputs ('left_halo') and
+        the right-halo wait before the correlator ('right_halo').  The first
+        event completes when the stream's previous work has, the second when
+        the wait is satisfied, so their difference is the GPU time the stream
+        stalls on the exchange -- measured, not inferred.  Off (None) by
+        default; reset by each call."""
+        self._wt = {"gather": [], "left_halo": [], "right_halo": []} if on else None
+
+    def _waited(self, name, wait, *a):
+        if self._wt is None:
+            return wait(*a)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = wait(*a)
+        e1.record()
+        self._wt[name].append((e0, e1))
+        return r
+
+    def wait_ms(self, steps: int | None = None):
+        """{wait: mean exposed ms per step} of the recorded steps (waits that a
+        rank does not have, e.g. rank 0's left halo, count as 0); synchronises."""
+        out = {}
+        for k, evs in (self._wt or {}).items():
+            if evs:
+                evs[-1][1].synchronize()
+            tot = sum(a.elapsed_time(b) for a, b in evs)
+            out[k] = tot / steps if steps else (tot / len(evs) if evs else 0.0)
+        return out
+
     def _begin_step(self):
         self._slot ^= 1
         work, self._gather[self._slot] = self._gather[self._slot], None
-        self.tr.wait(work)                # the all-gather two steps back (long done)
+        if work:
+            self._waited("gather", self.tr.wait, work)   # the all-gather two steps back
 
     def _gather_peaks(self):
         rows = self._rows[self._slot]
@@ -268,7 +309,7 @@ class StreamChain:
         s = -(-hist // D) * D
         if s < n:
             run(s, n)
-        self._exchange_wait(reqs)
+        self._waited("left_halo", self._exchange_wait, reqs)
         run(0, min(s, n))
 
     def step(self):
@@ -289,19 +330,29 @@ class StreamChain:
                                         self.y_ext[ny: ny + L - 1] if r < w - 1 else None,
                                         r + 1 if r < w - 1 else None)
         be.psd_into(self.y_ext[: ny], self.sxx)
-        self._exchange_wait(reqs)
+        if reqs or (w > 1 and L > 1):
+            self._waited("right_halo", self._exchange_wait, reqs)
         if L:
             halo = (L - 1) if r < w - 1 else 0
             be.xcorr_peak(self.y_ext[: ny + halo], self.rec)
             self.peak_rows = self._gather_peaks() if w > 1 else [self.rec]
 
     def global_peak(self):
-        """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step."""
+        """(max |c|, global lag, sum |c|, sum |c|^2, n_outputs) of the last step.
+        A refine fault -- on this rank since the last call (the backend's
+        sticky fault word) or on any rank (its gathered row's poisoned index,
+        refine.hip poison_record) -- raises RefineFault."""
         self.tr.wait(self._gather[self._slot])
+        check = getattr(self.be, "check_refine", None)
+        if check is not None:
+            check()
         rows = []
         for r, t in enumerate(self.peak_rows):
             h = t.detach().cpu().reshape(4)
             idx = int(h.view(torch.int64)[1].item())
+            if idx < 0:
+                from ._lib import RefineFault
+                raise RefineFault(f"exact-argmax refine faulted on rank {r} (poisoned peak record)")
             rows.append((float(h[0]), r * self.ny + idx, float(h[2]), float(h[3])))
         m, i, s1, s2 = combine_peaks(np.array(rows, dtype=object))
         nout = self.world * self.ny - self.L + 1
@@ -408,7 +459,11 @@ class NativeChain:
         pk, nout = Peak(), C.c_int64()
         rc = self.ctx.lib.vsig_chain_result(self.h, C.byref(pk), C.byref(nout))
         if rc:
-            raise RuntimeError(f"vsig_chain_result: {rc}")
+            msg = self.ctx.lib.vsig_chain_last_error(self.h).decode()
+            if rc == -6:                   # VSIG_E_REFINE: the exact-argmax contract broke
+                from ._lib import RefineFault
+                raise RefineFault(f"vsig_chain_result: {msg}")
+            raise RuntimeError(f"vsig_chain_result: {rc}: {msg}")
         return pk.peak, int(pk.index), pk.sum_abs, pk.sum_abs2, int(nout.value)
 
     def __del__(self):
