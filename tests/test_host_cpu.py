@@ -162,3 +162,23 @@ def test_c_examples_compile(tmp_path, name):
     chain over the loopback / RCCL transports) link against the library's
     exported symbols (the non-Python binding of INTEGRATION.md)."""
     assert os.path.exists(_build_c_example(str(tmp_path / name), name))
+
+
+def test_numpy_blas_threads_tracks_limits():
+    """The refine's OpenBLAS thread count follows threadpool_limits at every
+    call, through a controller found once (no per-call library rescan: ADVICE
+    r04 -- threadpool_info() costs milliseconds)."""
+    import time
+    from threadpoolctl import threadpool_info, threadpool_limits
+    from vector_amd._lib import numpy_blas_threads
+    want = [d["num_threads"] for d in threadpool_info() if d.get("internal_api") == "openblas"]
+    if not want:
+        pytest.skip("numpy without OpenBLAS")
+    assert numpy_blas_threads() == want[0]
+    with threadpool_limits(1):
+        assert numpy_blas_threads() == 1
+    assert numpy_blas_threads() == want[0]
+    t0 = time.perf_counter()
+    for _ in range(200):
+        numpy_blas_threads()
+    assert (time.perf_counter() - t0) / 200 < 1e-3

@@ -11,6 +11,12 @@ from vector_amd import _build  # noqa: E402
 VARIANTS = {
     "libvsig_rtrace": ("VSIG_REFINE_TRACE=1",),
 }
-for name in (sys.argv[1:] or VARIANTS):
-    _build.build(defines=VARIANTS[name], out=os.path.join(_build.HERE, name + ".so"), verbose=False)
+# name -> {source: extra compiler flags} (code-generation A/Bs)
+FLAG_VARIANTS = {
+    "libvsig_xilp": {"xcorr.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
+    "libvsig_xbias": {"xcorr.hip": ["-mllvm", "-amdgpu-schedule-metric-bias=0"]},
+}
+for name in (sys.argv[1:] or list(VARIANTS) + list(FLAG_VARIANTS)):
+    _build.build(defines=VARIANTS.get(name, ()), src_flags=FLAG_VARIANTS.get(name),
+                 out=os.path.join(_build.HERE, name + ".so"), verbose=False)
     print("built", name)

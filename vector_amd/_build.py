@@ -48,32 +48,80 @@ def _stale() -> bool:
     return open(stamp).read().strip() != source_hash()
 
 
-def build(force: bool = False, verbose: bool = True, defines=(), out: str = LIB) -> str:
-    """Compile every HIP source into vector_amd/libvsig.so (gfx950).  `defines`
-    / `out` build A/B variants (e.g. VSIG_SCALAR_FFT -> libvsig_scalar.so,
-    loaded with VSIG_LIB=... by the tuning tools; never by the product)."""
-    if out == LIB and not defines and not force and not _stale():
-        return LIB
+# objects are cached by (compiler, flags, sources -- the source hash is one of
+# the flags): A/B variants that change one translation unit's flags recompile
+# only that one
+OBJDIR = os.path.join(ROOT, "build", "objcache")
+
+
+def _compiler(defines=(), src=None):
+    """hipcc and its flags for one source (the build id goes into vsig_api.hip
+    alone, so an edit elsewhere recompiles only the edited unit and the API)."""
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
              "-fno-slp-vectorize",   # SLP packs f32 pairs into v_pk_* + v_mov shuffles
-             "-Wall", "-Wno-unused-function", f'-DVSIG_SRC_HASH="{source_hash()}"',
-             *[f"-D{d}" for d in defines]]
-    objdir = os.path.join(ROOT, "build", os.path.basename(out) + ".obj")
-    os.makedirs(objdir, exist_ok=True)
+             "-Wall", "-Wno-unused-function", *[f"-D{d}" for d in defines]]
+    if src == "vsig_api.hip":
+        flags.append(f'-DVSIG_SRC_HASH="{source_hash()}"')
+    return hipcc, flags
+
+
+def _unit_hash(src: str) -> str:
+    """The source and every shared header (any header edit recompiles all)."""
+    h = hashlib.sha256()
+    for f in [src, *HEADERS]:
+        h.update(open(os.path.join(CSRC, f), "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "vsig.h"), "rb").read())
+    return h.hexdigest()
+
+
+def object_path(src: str, defines=(), extra=()) -> str:
+    """The cached object of one source under these defines / extra flags
+    (tests read the product's device code from it: tests/test_isa_cpu.py)."""
+    hipcc, flags = _compiler(defines, src)
+    key = hashlib.sha256(" ".join([hipcc, *flags, *extra, _unit_hash(src)]).encode()).hexdigest()[:16]
+    return os.path.join(OBJDIR, f"{src}.{key}.o")
+
+
+def compile_object(src: str) -> str:
+    """The product object of one source (compiled into the cache if missing)."""
+    obj = object_path(src)
+    if not os.path.exists(obj):
+        hipcc, flags = _compiler((), src)
+        os.makedirs(OBJDIR, exist_ok=True)
+        subprocess.run([hipcc, *flags, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"], check=True)
+        os.replace(obj + ".tmp", obj)
+    return obj
+
+
+def build(force: bool = False, verbose: bool = True, defines=(), out: str = LIB, src_flags=None) -> str:
+    """Compile every HIP source into vector_amd/libvsig.so (gfx950).  `defines`
+    / `out` build A/B variants (e.g. VSIG_SCALAR_FFT -> libvsig_scalar.so,
+    loaded with VSIG_LIB=... by the tuning tools; never by the product);
+    src_flags: {source: [extra compiler flags]} for an A/B of code generation."""
+    src_flags = src_flags or {}
+    if out == LIB and not defines and not src_flags and not force and not _stale():
+        return LIB
+    os.makedirs(OBJDIR, exist_ok=True)
 
     def compile_one(src):
-        obj = os.path.join(objdir, src + ".o")
-        cmd = [hipcc, *flags, "-c", os.path.join(CSRC, src), "-o", obj]
+        extra = list(src_flags.get(src, ()))
+        obj = object_path(src, defines, extra)
+        if os.path.exists(obj) and not force:
+            return obj
+        hipcc, flags = _compiler(defines, src)
+        cmd = [hipcc, *flags, *extra, "-c", os.path.join(CSRC, src), "-o", obj + ".tmp"]
         if verbose:
             print(" ".join(cmd), file=sys.stderr)
         subprocess.run(cmd, check=True)
+        os.replace(obj + ".tmp", obj)
         return obj
 
     jobs = int(os.environ.get("MAX_JOBS", "0")) or min(len(SOURCES), os.cpu_count() or 1)
     with ThreadPoolExecutor(max_workers=max(1, min(jobs, 16))) as ex:
         objs = list(ex.map(compile_one, SOURCES))
     tmp = out + ".tmp"
+    hipcc = _compiler()[0]
     cmd = [hipcc, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp]
     if verbose:
         print(" ".join(cmd), file=sys.stderr)

@@ -162,33 +162,43 @@ def load_library(path: str | None = None):
 
 
 _warned_no_threadpoolctl = False
+_blas_ctl = None            # threadpoolctl controller of numpy's OpenBLAS (found once)
 
 
 def numpy_blas_threads() -> int:
     """The thread count of the OpenBLAS behind this process's numpy (its zdotu
     splits a complex128 dot of more than 10000 terms into that many chunks,
     which decides the rounding of np.correlate's long sums); read at every call
-    (threadpool_limits / OPENBLAS_NUM_THREADS may change it).  1 if unknown --
-    with a warning when threadpoolctl is missing: correlations with more than
-    10000 overlap terms then match numpy only if its OpenBLAS runs one thread."""
-    global _warned_no_threadpoolctl
-    try:
-        from threadpoolctl import threadpool_info
-    except ImportError:
-        if not _warned_no_threadpoolctl:
-            import warnings
-            warnings.warn("threadpoolctl is not importable: numpy's OpenBLAS thread count is "
-                          "taken as 1 for the exact argmax of correlations over 10000 terms",
-                          RuntimeWarning, stacklevel=2)
-            _warned_no_threadpoolctl = True
+    (threadpool_limits / OPENBLAS_NUM_THREADS may change it) through a
+    controller found once (threadpool_info() rescans every loaded library:
+    ~5 ms a call; the controller's get_num_threads is one C call into
+    OpenBLAS).  1 if unknown -- with a warning when threadpoolctl is missing:
+    correlations with more than 10000 overlap terms then match numpy only if
+    its OpenBLAS runs one thread."""
+    global _warned_no_threadpoolctl, _blas_ctl
+    if _blas_ctl is None:
+        try:
+            import numpy  # noqa: F401  (its OpenBLAS is loaded with it)
+            from threadpoolctl import ThreadpoolController
+        except ImportError:
+            if not _warned_no_threadpoolctl:
+                import warnings
+                warnings.warn("threadpoolctl is not importable: numpy's OpenBLAS thread count is "
+                              "taken as 1 for the exact argmax of correlations over 10000 terms",
+                              RuntimeWarning, stacklevel=2)
+                _warned_no_threadpoolctl = True
+            return 1
+        try:
+            ctl = [lc for lc in ThreadpoolController().lib_controllers if lc.internal_api == "openblas"]
+        except Exception:
+            ctl = []
+        _blas_ctl = ctl[0] if ctl else False
+    if not _blas_ctl:
         return 1
     try:
-        for d in threadpool_info():
-            if d.get("internal_api") == "openblas":
-                return max(1, min(1024, int(d.get("num_threads", 1))))
+        return max(1, min(1024, int(_blas_ctl.get_num_threads())))
     except Exception:
-        pass
-    return 1
+        return 1
 
 
 class Context:

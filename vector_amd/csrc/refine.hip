@@ -987,8 +987,11 @@ __global__ __launch_bounds__(kNpThreads, 2) void refine_fused(
   __syncthreads();
   const long long tk = stk;
   if (tk < g1) {
+    // keys + items completed before (stores_done in finalize_select_block); the
+    // flag goes up by an atomic add, so every hand-off signal of this file is
+    // one global_atomic_add behind a drained vmcnt (tools/isa_handoffs.py)
     if (finalize_select_block(f, (int)tk, g1) && tid == 0)
-      st_agent(&fc->flag, 1ull);                   // keys + items completed before
+      atomicAdd(&fc->flag, 1ull);
     return;
   }
   const long long vb = tk - g1;

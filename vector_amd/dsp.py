@@ -589,8 +589,11 @@ class Correlator:
 
     def __call__(self, s: torch.Tensor, mode="valid", out: torch.Tensor | None = None,
                  peak: torch.Tensor | None = None):
-        """Enqueue; returns (c or None, peak buffer (device vsig_peak_t))."""
+        """Enqueue; returns (c or None, peak buffer (device vsig_peak_t)).  The
+        refine matches numpy's current OpenBLAS thread count, as the numpy
+        front end does (Context.sync_blas_threads: one C call)."""
         self.ctx.bind_stream()
+        self.ctx.sync_blas_threads()
         _check_dev(s, 1, torch.complex64, "correlator stream", self.ctx.device)
         if mode not in ("valid", "full"):
             raise ValueError("Correlator supports mode 'valid' and 'full'")
