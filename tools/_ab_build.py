@@ -13,8 +13,6 @@ VARIANTS = {
 }
 # name -> {source: extra compiler flags} (code-generation A/Bs)
 FLAG_VARIANTS = {
-    "libvsig_xilp": {"xcorr.hip": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"]},
-    "libvsig_xbias": {"xcorr.hip": ["-mllvm", "-amdgpu-schedule-metric-bias=0"]},
 }
 for name in (sys.argv[1:] or list(VARIANTS) + list(FLAG_VARIANTS)):
     _build.build(defines=VARIANTS.get(name, ()), src_flags=FLAG_VARIANTS.get(name),
