@@ -62,7 +62,17 @@ typedef struct vsig_fir vsig_fir;
 typedef struct vsig_xcorr vsig_xcorr;
 
 /* Result of a |c| peak reduction (find_correlation_peak, utils.py:1321-1334).
- * index: first maximum of |c|; peak: |c[index]|; sums over every element. */
+ * index: first maximum of |c|; peak: |c[index]|; sums over every element.
+ * From the fused correlators (a peak record without a stored c) the sums are
+ * fp32 per-thread sums of the fp32 |c|, combined in double: relative error
+ * ~1e-7, so the single-pass variance var = sum_abs2/n - (sum_abs/n)^2 carries
+ * ~1e-7 x (sum_abs2/n) / var.  find_correlation_peak's confidence formed from
+ * them is within 1e-5 of numpy's while var >= 0.05 sum_abs2/n (noise-like
+ * |c|: 0.21); below that (a flat |c|: a tone, a tone under weak noise) use
+ * vsig_correlate_stats_dev for numpy's own mean / std -- the Python front end
+ * (correlate_peak) does exactly that (tests/test_gpu_refine.py, tone under
+ * noise at 0-60 dB).  An index of -1 means the record is invalid (a refine
+ * fault, VSIG_E_REFINE / vsig_refine_status 3). */
 typedef struct vsig_peak_t {
   double peak;
   int64_t index;
