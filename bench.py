@@ -200,6 +200,18 @@ WORKLOADS = {
 }
 
 
+def rehearsal_env(rank: int) -> dict:
+    """--rehearse-one-gpu: every rank on cuda:0 of a one-GPU box (the pool's),
+    over the production RCCL path.  RCCL refuses two ranks on one device of one
+    host, so each rank names its own host (NCCL_HOSTID) and the ranks talk over
+    RCCL's socket transport on loopback (P2P / SHM off).  Exercises every RCCL
+    call, stream dependency and the per-rank line of an N-GPU run; its times are
+    N ranks sharing one GPU and sockets for xGMI -- not a scaling measurement
+    (tests/test_gpu_rccl.py, tests/test_gpu_bench.py)."""
+    return {"NCCL_HOSTID": f"vsig-rank{rank}", "NCCL_SOCKET_IFNAME": "lo", "NCCL_NET": "Socket",
+            "NCCL_P2P_DISABLE": "1", "NCCL_SHM_DISABLE": "1", "LOCAL_RANK": "0"}
+
+
 def launch_ranks(n: int, argv: list[str]) -> int:
     """`bench.py --gpus N` without a launcher: start N child processes of this
     script (one per GPU, RANK = LOCAL_RANK = r, WORLD_SIZE = N, rendezvous on
@@ -221,10 +233,13 @@ def launch_ranks(n: int, argv: list[str]) -> int:
     old = signal.signal(signal.SIGTERM, _term)
     rc = 0
     try:
+        rehearse = "--rehearse-one-gpu" in argv
         for r in range(n):
             env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
                        LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=port,
                        TORCHELASTIC_USE_AGENT_STORE="True", TORCHELASTIC_RESTART_COUNT="0")
+            if rehearse:
+                env.update(rehearsal_env(r))
             procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *argv],
                                           env=env))
         live = list(procs)
@@ -500,6 +515,9 @@ def main():
     ap.add_argument("--c2-steps", type=int, default=10)
     ap.add_argument("--c2-samples", type=int, default=1 << 28)
     ap.add_argument("--launcher-selftest", default=None, help=argparse.SUPPRESS)
+    ap.add_argument("--rehearse-one-gpu", action="store_true",
+                    help="N ranks on cuda:0 over RCCL sockets (functional rehearsal of the N-GPU "
+                         "path on a one-GPU box; not a scaling number)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -598,6 +616,9 @@ def main():
         "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
         "ranks": leg["ranks"],
     }
+    if args.rehearse_one_gpu:
+        out["rehearsal"] = (f"{world} ranks on one GPU over RCCL's socket transport: a functional "
+                            f"run of the N-GPU path, not a scaling measurement")
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -786,6 +807,9 @@ def run_pfb(args, world, rank, local, dev):
         "check": {"frame1_rel_err": err, "ok": err < 1e-5},
         "rccl_world": dist.get_world_size() if dist.is_initialized() else 1,
     }
+    if args.rehearse_one_gpu:
+        out["rehearsal"] = (f"{world} ranks on one GPU over RCCL's socket transport: a functional "
+                            f"run of the N-GPU path, not a scaling measurement")
     print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
