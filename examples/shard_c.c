@@ -5,9 +5,14 @@
  *
  *   ./shard_c loopback W            W ranks as threads of this process, all on
  *                                   device 0 (in-process loopback transport)
- *   ./shard_c rccl RANK WORLD FILE  one rank per process and GPU over RCCL:
+ *   ./shard_c rccl RANK WORLD FILE [DEVICE]
+ *                                   one rank per process and GPU over RCCL:
  *                                   rank 0 writes the RCCL unique id to FILE,
- *                                   the others wait for it (one node)
+ *                                   the others wait for it (one node); DEVICE
+ *                                   (default RANK) puts every rank on one GPU
+ *                                   for a one-GPU rehearsal (each rank then
+ *                                   needs its own NCCL_HOSTID: RCCL's socket
+ *                                   transport, tests/test_gpu_native_chain.py)
  *
  * Every rank synthesises its own chunk of one capture (tones + LCG noise seeded
  * by the global sample index, a QPSK preamble planted at K0) and prints the
@@ -150,6 +155,7 @@ int main(int argc, char** argv) {
   if (argc >= 5 && !strcmp(argv[1], "rccl")) {
     const int rank = atoi(argv[2]), world = atoi(argv[3]);
     const char* file = argv[4];
+    const int device = argc >= 6 ? atoi(argv[5]) : rank;
     design(world);
     char id[128];
     if (rank == 0) {
@@ -173,13 +179,13 @@ int main(int argc, char** argv) {
       fclose(f);
     }
     void* comm = NULL;
-    if (vsig_rccl_comm_init(world, rank, id, rank, &comm)) { fprintf(stderr, "comm init failed\n"); return 2; }
-    struct rank_args a = {rank, world, rank, {0}, 1, 0};
+    if (vsig_rccl_comm_init(world, rank, id, device, &comm)) { fprintf(stderr, "comm init failed\n"); return 2; }
+    struct rank_args a = {rank, world, device, {0}, 1, 0};
     if (vsig_rccl_transport(comm, &a.tr)) return 2;
     run_rank(&a);
     vsig_rccl_comm_destroy(comm);
     return a.ok ? 0 : 1;
   }
-  fprintf(stderr, "usage: shard_c loopback W | shard_c rccl RANK WORLD IDFILE (a fresh path per run)\n");
+  fprintf(stderr, "usage: shard_c loopback W | shard_c rccl RANK WORLD IDFILE [DEVICE] (a fresh IDFILE per run)\n");
   return 2;
 }

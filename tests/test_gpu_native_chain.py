@@ -209,3 +209,37 @@ def test_c_shard_example_rccl_world1(gpu, tmp_path):
     if r.returncode == 2 and "no RCCL" in r.stderr:
         pytest.skip("librccl not found")
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_c_shard_example_rccl_world2_one_gpu(gpu, tmp_path):
+    """examples/shard_c.c over RCCL at world 2 from plain C (ncclSend / ncclRecv
+    halos and ncclAllGather peaks through vsig_rccl_transport), both ranks on
+    this box's one GPU: each process names its own NCCL_HOSTID, so RCCL runs its
+    socket transport on loopback (bench.rehearsal_env).  Exit 0 on both = every
+    rank found the preamble at its global lag."""
+    import os
+    import subprocess
+    import sys
+    from test_host_cpu import _build_c_example
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    exe = _build_c_example(str(tmp_path / "shard_c"), "shard_c")
+    uid = str(tmp_path / "uid2")
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, **bench.rehearsal_env(r))
+        procs.append(subprocess.Popen([exe, "rccl", str(r), "2", uid, "0"], env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=150)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, o, e))
+    if any(rc == 2 and "no RCCL" in e for rc, _, e in outs):
+        pytest.skip("librccl not found")
+    assert all(rc == 0 for rc, _, _ in outs), outs
+    assert sum(o.count("global peak") for _, o, _ in outs) == 2
