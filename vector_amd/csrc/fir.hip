@@ -1,6 +1,10 @@
 // Overlap-save FIR kernel (gfx950), decimation folded into the store (filter).
 #include "os_common.hpp"
 
+#ifndef VSIG_FIR1_LO16
+#define VSIG_FIR1_LO16 0   // A/B: line-aligned D = 1 output runs (launch_fir_os)
+#endif
+
 namespace vsig {
 
 // Store the valid outputs of FIR block b (conj undoes the inverse-by-conj
@@ -74,17 +78,18 @@ __device__ __forceinline__ void fir_store_x4(const float2* v, float2* __restrict
 // Two consecutive blocks per workgroup (fft_pair: the LDS stores of one
 // segment overlap the other's butterflies), twiddles from register anchors.
 // MIX: the NCO mixer applied to every loaded sample (vsig_fir_exec_mix_dev).
+// lo: the segment's offset before its block's first output (>= ntaps - 1, and
+// lo + hop <= M): outputs are the circular indices [lo, lo + hop).
 template <class P, bool MIX = false, bool X4 = false, bool XS = false>
 __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
-    int ntaps, long long hop, int decim, float2* __restrict__ y, long long nblocks,
+    int lo, long long hop, int decim, float2* __restrict__ y, long long nblocks,
     const float2* __restrict__ tw, MixArgs mix) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   __shared__ float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (2 * b >= nblocks) return;  // uniform per block
-  const int lo = ntaps - 1;
   const long long nloc = n - g0;
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
@@ -373,24 +378,35 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
     using PL = decltype(plan);
     if constexpr (PL::TF == 64) {
       if (mix) {
-        hipLaunchKernelGGL((fir_os_kernel<PL, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps,
+        hipLaunchKernelGGL((fir_os_kernel<PL, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps - 1,
                            hop, decim, y, nblocks, tw, m);
         return;
       }
     }
     if constexpr (map0_of<PL>::value == kMapPair) {
-      const bool xs = decim == 1 && (ntaps - 1) % 2 == 0 && x4_aligned(y, 0, hop);
-      if (x4_aligned(x, g0 - (ntaps - 1), hop)) {
+      // the pair map's 16-byte stores write 128-output runs at circular
+      // indices 128 i: with lo a multiple of 16 every run fills whole 128-byte
+      // lines of y (one store instruction per line) -- the segment then starts
+      // a few samples earlier (lo >= ntaps - 1 and lo + hop <= M still hold),
+      // and a history of a multiple of 16 (the chain's x_ext) keeps the loads
+      // line-aligned as well
+      int lo = ntaps - 1;
+#if VSIG_FIR1_LO16
+      const int lo16 = (lo + 15) & ~15;
+      if (decim == 1 && lo16 + hop <= PL::N && x4_aligned(x, g0 - lo16, hop)) lo = lo16;
+#endif
+      const bool xs = decim == 1 && lo % 2 == 0 && x4_aligned(y, 0, hop);
+      if (x4_aligned(x, g0 - lo, hop)) {
         if (xs)
           hipLaunchKernelGGL((fir_os_kernel<PL, false, true, true>), grid, dim3(PL::TF), 0, st, x, n, g0,
-                             Hs, ntaps, hop, decim, y, nblocks, tw, m);
+                             Hs, lo, hop, decim, y, nblocks, tw, m);
         else
           hipLaunchKernelGGL((fir_os_kernel<PL, false, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs,
-                             ntaps, hop, decim, y, nblocks, tw, m);
+                             lo, hop, decim, y, nblocks, tw, m);
         return;
       }
     }
-    hipLaunchKernelGGL((fir_os_kernel<PL, false>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps,
+    hipLaunchKernelGGL((fir_os_kernel<PL, false>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps - 1,
                        hop, decim, y, nblocks, tw, m);
   };
   switch (M) {
