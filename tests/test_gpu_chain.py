@@ -59,14 +59,16 @@ def test_split_first_fir_matches_single_launch(gpu, decim):
     cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=1024, template=None)
     be = HipBackend(cfg, 0)
     ch = StreamChain(cfg, be, 0, 1)
-    x_ext = torch.from_numpy(ref.synth_iq(n + 254, seed=5)).cuda()
+    h = ch.hist                      # 254 taps' history rounded up to 16: 256
+    assert h == 256
+    x_ext = torch.from_numpy(ref.synth_iq(n + h, seed=5)).cuda()
     ch.x_ext.copy_(x_ext)
     want = torch.empty(n // decim, dtype=torch.complex64, device="cuda")
-    be.fir_into(x_ext, 254, want)
+    be.fir_into(x_ext[h - 254:], 254, want)          # the minimal history: the same stream
     # the split as _fir_first issues it (exchange skipped: the halo is already in place)
-    s = -(-254 // decim) * decim
-    be.fir_into(ch.x_ext[s: n + 254], 254, ch.y_ext[s // decim: n // decim])
-    be.fir_into(ch.x_ext[: s + 254], 254, ch.y_ext[: s // decim])
+    s = -(-h // decim) * decim
+    be.fir_into(ch.x_ext[s: n + h], h, ch.y_ext[s // decim: n // decim])
+    be.fir_into(ch.x_ext[: s + h], h, ch.y_ext[: s // decim])
     torch.cuda.synchronize()
     got = ch.y.cpu().numpy()
     w = want.cpu().numpy()

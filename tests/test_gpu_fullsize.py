@@ -108,11 +108,11 @@ def test_c5_shape_decimated_chain(gpu):
 
 def test_c5_headline_size_2pow31(gpu):
     """The headline's own per-GPU size (BASELINE configs[4] on one GPU, what
-    bench.py times): 2**31 input samples (x_ext = 2**31 + 254 with the FIR
+    bench.py times): 2**31 input samples (x_ext = 2**31 + 256 with the FIR
     history, past the 32-bit index range), D = 4.  FIR outputs and PSD frames
     of the first, a middle and the last 8192 decimated outputs against the
     oracle on those input slices with their halos (the last slice reads input
-    samples up to 2**31 - 1, x_ext offsets up to 2**31 + 253); a preamble
+    samples up to 2**31 - 1, x_ext offsets up to 2**31 + 255); a preamble
     planted in the tail of the capture (input sample ~2**31 - 2**18) is found
     at its exact lag, with numpy's |c| (the direct double-precision dot)."""
     n, decim = 1 << 31, 4

@@ -10,7 +10,6 @@ from vector_amd import _build  # noqa: E402
 # recorded in DESIGN.md, see round 3's list)
 VARIANTS = {
     "libvsig_rtrace": ("VSIG_REFINE_TRACE=1",),
-    "libvsig_lo16": ("VSIG_FIR1_LO16=1",),
 }
 # name -> {source: extra compiler flags} (code-generation A/Bs)
 FLAG_VARIANTS = {

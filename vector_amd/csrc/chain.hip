@@ -103,7 +103,7 @@ int vsig_chain_create(vsig_ctx* ctx, const vsig_chain_config* cfg, int32_t rank,
   ch->decim = (int)D;
   ch->nfft = (int)nfft;
   ch->ny = n / D;
-  ch->hist = cfg->ntaps - 1;
+  ch->hist = (cfg->ntaps - 1 + 15) / 16 * 16;   // 128-byte-aligned segment starts (shard.py)
   ch->L = cfg->tmpl ? cfg->L : 0;
   ch->scale = cfg->psd_scale;
   if (world > 1 && (n < ch->hist || (ch->L && ch->ny < ch->L - 1))) {

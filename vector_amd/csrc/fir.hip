@@ -1,10 +1,6 @@
 // Overlap-save FIR kernel (gfx950), decimation folded into the store (filter).
 #include "os_common.hpp"
 
-#ifndef VSIG_FIR1_LO16
-#define VSIG_FIR1_LO16 0   // A/B: line-aligned D = 1 output runs (launch_fir_os)
-#endif
-
 namespace vsig {
 
 // Store the valid outputs of FIR block b (conj undoes the inverse-by-conj
@@ -385,16 +381,15 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
     }
     if constexpr (map0_of<PL>::value == kMapPair) {
       // the pair map's 16-byte stores write 128-output runs at circular
-      // indices 128 i: with lo a multiple of 16 every run fills whole 128-byte
-      // lines of y (one store instruction per line) -- the segment then starts
-      // a few samples earlier (lo >= ntaps - 1 and lo + hop <= M still hold),
-      // and a history of a multiple of 16 (the chain's x_ext) keeps the loads
-      // line-aligned as well
+      // indices 128 i: with lo a multiple of 16 every run covers whole 128-byte
+      // lines of y (one store instruction per line, none split between two) --
+      // the segment then starts a few samples earlier (lo >= ntaps - 1 and
+      // lo + hop <= M still hold).  Config 2 (255 taps, lo 254 -> 256): FIR
+      // 0.822 -> 0.789 ms (profiles/r05_fir_align_ab.txt); the loads' own
+      // alignment (the chain's 16-multiple history) measured neutral at D = 1.
       int lo = ntaps - 1;
-#if VSIG_FIR1_LO16
       const int lo16 = (lo + 15) & ~15;
       if (decim == 1 && lo16 + hop <= PL::N && x4_aligned(x, g0 - lo16, hop)) lo = lo16;
-#endif
       const bool xs = decim == 1 && lo % 2 == 0 && x4_aligned(y, 0, hop);
       if (x4_aligned(x, g0 - lo, hop)) {
         if (xs)

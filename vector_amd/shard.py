@@ -30,7 +30,6 @@ tests/test_gpu_shard_threads.py).
 from __future__ import annotations
 
 from dataclasses import dataclass
-import os
 
 import numpy as np
 import torch
@@ -197,9 +196,11 @@ class StreamChain:
         cfg.validate(world)
         self.cfg, self.be, self.rank, self.world, self.group = cfg, backend, rank, world, group
         self.tr = transport if transport is not None else TorchTransport(group)
-        self.hist = len(cfg.taps) - 1
-        if os.environ.get("VSIG_CHAIN_HIST16", "0") == "1":   # A/B: line-aligned FIR loads
-            self.hist = (self.hist + 15) // 16 * 16
+        # the left halo: ntaps - 1 samples, rounded up to a multiple of 16 so
+        # that [halo | chunk] puts the FIR's segment starts on 128-byte lines
+        # (D = 4: lo2 = 256 at 255 taps; the surplus samples are never read by
+        # a tap; profiles/r05_fir_align_ab.txt)
+        self.hist = (len(cfg.taps) - 1 + 15) // 16 * 16
         self.ny = cfg.n_local // cfg.decim
         self.L = len(cfg.template) if cfg.template is not None else 0
         self.yhalo = (self.L - 1) if (self.L and rank < world - 1) else 0
