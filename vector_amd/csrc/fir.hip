@@ -1,7 +1,6 @@
 // Overlap-save FIR kernel (gfx950), decimation folded into the store (filter).
 #include "os_common.hpp"
 
-
 namespace vsig {
 
 // Store the valid outputs of FIR block b (conj undoes the inverse-by-conj
