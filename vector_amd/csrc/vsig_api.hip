@@ -833,7 +833,11 @@ static int fir_exec(vsig_fir* f, const void* x, int64_t nhist, int64_t n, void* 
     // decimation in the frequency domain: M/D-point inverse transforms
     const float2* twd;
     const int D = f->decim;
-    const int lo2 = (f->ntaps - 1 + D - 1) / D * D;
+    int lo2 = (f->ntaps - 1 + D - 1) / D * D;
+    // a multiple of 16 when the block allows (as fir_os_kernel's lo): the
+    // decimated output runs (64 per store instruction) then start on 128-byte
+    // lines, and so do the segments of a 16-multiple history (the chain's)
+    if (((lo2 + 15) & ~15) + 768 <= f->M) lo2 = (lo2 + 15) & ~15;
     const long long hop = (long long)(f->M - lo2) / D * D;
     if (hop < D) return fail(c, VSIG_E_UNSUPPORTED, "decim too large for the block size");
     if (f->G) {      // D = 4: polyphase form (fir_poly_kernel)
