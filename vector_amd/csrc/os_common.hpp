@@ -13,8 +13,8 @@ namespace vsig {
 // non-temporal hint where it measured faster on the chain: the PSD's frame
 // loads and the FIR's output stores (so the filtered stream does not sit in
 // L2 / the Infinity Cache as dirty lines while the PSD and the correlator
-// read it); the FIR's overlapping segment loads stay plain (NT measured
-// slower there).
+// read it), and the FIR pairs' rows no other pair reads (load_pair_x4); the
+// rows neighbouring pairs share stay plain (their second read is an L2 hit).
 template <bool NT = false>
 __device__ __forceinline__ float2 ld_stream(const float2* p) {
   if constexpr (NT) return fromv(__builtin_nontemporal_load(reinterpret_cast<const f2v*>(p)));
@@ -111,8 +111,18 @@ __device__ __forceinline__ void load_pair_x4(float2* a, float2* d, const float2*
     typedef float f4 __attribute__((ext_vector_type(4)));
     const f4* b4 = reinterpret_cast<const f4*>(x + s0);
     f4 u[P::E / 2 + 6];
+    // rows 0, 1 and 12, 13 are also read by the neighbouring pairs (their 256
+    // overlap samples, from L2); the rows only this pair reads are loaded
+    // non-temporal.  With the segment starts on 128-byte lines (the chain's
+    // 16-multiple halo) this took the D = 4 FIR 3.67 -> 3.57 ms at config 5
+    // (profiles/r05_fir_nt_ab.txt; all rows non-temporal, or all but 12 / 13:
+    // slower than plain; D = 1 neutral).  Before the alignment fix the same
+    // split measured neutral (r04_ab_neutral.txt item 1).
 #pragma unroll
-    for (int i = 0; i < P::E / 2 + 6; ++i) u[i] = b4[t + 64 * i];   // float4 rows 0..13
+    for (int i = 0; i < P::E / 2 + 6; ++i) {                      // float4 rows 0..13
+      if (i >= 2 && i < 12) u[i] = __builtin_nontemporal_load(b4 + t + 64 * i);
+      else u[i] = b4[t + 64 * i];
+    }
     auto unpack = [&](float2* v, int e, const f4& w) {
       const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.x), __float_as_uint(w.z), false, false);
       const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(w.y), __float_as_uint(w.w), false, false);
