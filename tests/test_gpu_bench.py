@@ -39,7 +39,7 @@ def test_bench_workload_small(gpu, workload):
         assert 0 < c2["fir+psd"]["hbm_frac"] < 1 and c2["samples"] == 1 << 21
 
 
-@pytest.mark.parametrize("world,workload", [(2, "c5"), (4, "c5"), (2, "c2"), (2, "pfb")])
+@pytest.mark.parametrize("world,workload", [(2, "c5"), (4, "c5"), (8, "c5"), (2, "c2"), (2, "pfb")])
 def test_bench_n_ranks_rehearsal_over_rccl(gpu, world, workload):
     """bench.py --gpus N end to end as the driver's N-GPU run executes it (its own
     launcher, one process per rank, torch.distributed over RCCL: halos by
