@@ -59,4 +59,10 @@ for v in range(40, 46):       # the same 4:1 pattern with LDS-DMA loads (global_
     name = f"read4to1_glds_u{U}" + ("_nt" if v & 1 else "")
     ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
     res[name] = (round(ms, 4), round(10 * n / ms / 1e6, 1))
+for v in range(50, 74):      # 4:1 with the lane width / unroll / both NT policies free
+    k = v - 50
+    W, U = (8, 4 << ((k % 12) // 4)) if k < 12 else (16, 2 << ((k % 12) // 4))
+    name = f"r4w{W}_u{U}" + ("_ntl" if k & 2 else "") + ("_nts" if k & 1 else "")
+    ms = t(lambda: ctx.check(ctx.lib.vsig_copy_bench(ctx.h, dsp._ptr(x), n, dsp._ptr(y), v, 0), "c"))
+    res[name] = (round(ms, 4), round(10 * n / ms / 1e6, 1))
 print(json.dumps(res))

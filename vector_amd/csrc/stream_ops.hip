@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <type_traits>
 
 #include "vsig_kernels.h"
 
@@ -310,8 +311,61 @@ __global__ __launch_bounds__(256) void reduce4_glds_probe(const f4v* __restrict_
   }
 }
 
+// The 4:1 read-mostly pattern with the load width, the unroll and both
+// non-temporal policies free (variants 50..): lanes of W bytes (8: float2,
+// 16: float4), U loads in flight per lane, one float2 store per 4 samples.
+template <int W, int U, bool NTL, bool NTS>
+__global__ __launch_bounds__(256) void reduce4w_probe(const float2* __restrict__ x, long long n,
+                                                      f2v* __restrict__ y) {
+  constexpr int S = W / 8;                        // samples per lane per load
+  typedef typename std::conditional<W == 16, f4v, f2v>::type V;
+  const V* xv = reinterpret_cast<const V*>(x);
+  const long long nv = n / S;
+  const long long base = ((long long)blockIdx.x * 256) * U + threadIdx.x;
+  V v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const long long i = base + (long long)u * 256;
+    v[u] = i < nv ? (NTL ? __builtin_nontemporal_load(xv + i) : xv[i]) : V{};
+  }
+  constexpr int G = 4 / S;                        // loads per output
+#pragma unroll
+  for (int u = 0; u < U; u += G) {
+    f2v s = {0.f, 0.f};
+#pragma unroll
+    for (int q = 0; q < G; ++q) {
+      if constexpr (W == 16) s += f2v{v[u + q].x + v[u + q].z, v[u + q].y + v[u + q].w};
+      else s += v[u + q];
+    }
+    const long long i = ((long long)blockIdx.x * 256) * (U / G) + threadIdx.x + (long long)(u / G) * 256;
+    if (i < n / 4) {
+      if constexpr (NTS) __builtin_nontemporal_store(s, y + i);
+      else y[i] = s;
+    }
+  }
+}
+
 hipError_t launch_copy_probe(const float2* x, long long n, float2* y, int variant, int grid,
                              hipStream_t st) {
+  if (variant >= 50 && variant < 74) {   // 50 + wi*12 + ui*4 + NTL*2 + NTS; W = 8 (U 4, 8, 16) / 16 (U 2, 4, 8)
+    const int k = variant - 50, wi = k / 12, ui = (k % 12) / 4, ntl = (k >> 1) & 1, nts = k & 1;
+    const int U = wi == 0 ? (4 << ui) : (2 << ui);
+    const long long per = 256LL * U * (wi == 0 ? 1 : 2);
+    const dim3 g((unsigned)((n + per - 1) / per)), b(256);
+    f2v* y2 = reinterpret_cast<f2v*>(y);
+#define VSIG_RW_(WW, UU)                                                                           \
+    if (ntl && nts) hipLaunchKernelGGL((reduce4w_probe<WW, UU, true, true>), g, b, 0, st, x, n, y2);   \
+    else if (ntl) hipLaunchKernelGGL((reduce4w_probe<WW, UU, true, false>), g, b, 0, st, x, n, y2);    \
+    else if (nts) hipLaunchKernelGGL((reduce4w_probe<WW, UU, false, true>), g, b, 0, st, x, n, y2);    \
+    else hipLaunchKernelGGL((reduce4w_probe<WW, UU, false, false>), g, b, 0, st, x, n, y2);
+    if (wi == 0) {
+      if (U == 4) { VSIG_RW_(8, 4) } else if (U == 8) { VSIG_RW_(8, 8) } else { VSIG_RW_(8, 16) }
+    } else {
+      if (U == 2) { VSIG_RW_(16, 2) } else if (U == 4) { VSIG_RW_(16, 4) } else { VSIG_RW_(16, 8) }
+    }
+#undef VSIG_RW_
+    return hipGetLastError();
+  }
   if (variant >= 40) {      // LDS-DMA read-mostly probes: 40 + (U index)*2 + NT, U = 2, 4, 8
     const int ui = (variant - 40) / 2, nt = variant & 1;
     const long long n4 = n / 2;
