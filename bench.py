@@ -160,16 +160,20 @@ def xcorr_block(L):
 
 def practical_ceiling(kind):
     """The best rate the pool's boxes reached on an access pattern like the
-    kernel's (tools/membw.py probes, profiles/r02_membw.json): 'read4to1' for
-    the decimating FIR's 8 B read : 2 B written per sample, 'copy' (16-byte
+    kernel's (tools/membw.py probes, the newest profiles/r0N_membw.json):
+    'read4to1' for the decimating FIR's 8 B read : 2 B written per sample
+    (every lane width / unroll / non-temporal variant of it), 'copy' (unrolled
     lanes, loads in flight, NT hints) for the 1:1 streams.  (GB/s, source)"""
-    try:
-        d = json.load(open(os.path.join(ROOT, "profiles", "r02_membw.json")))
-    except Exception:
-        return None
-    pref = "read4to1" if kind == "read4to1" else "probe_u"
-    vals = [v[1] for k, v in d.items() if k.startswith(pref) and isinstance(v, list)]
-    return (max(vals), f"profiles/r02_membw.json max({pref}*)") if vals else None
+    for name in ("r05_membw.json", "r02_membw.json"):
+        try:
+            d = json.load(open(os.path.join(ROOT, "profiles", name)))
+        except Exception:
+            continue
+        prefs = ("read4to1", "r4w") if kind == "read4to1" else ("probe_u",)
+        vals = [v[1] for k, v in d.items() if k.startswith(prefs) and isinstance(v, list)]
+        if vals:
+            return max(vals), f"profiles/{name} max({'|'.join(p + '*' for p in prefs)})"
+    return None
 
 
 def load_traffic(key):
