@@ -182,3 +182,17 @@ def test_numpy_blas_threads_tracks_limits():
     for _ in range(200):
         numpy_blas_threads()
     assert (time.perf_counter() - t0) / 200 < 1e-3
+
+
+def test_bench_practical_ceiling_uses_newest_probe():
+    """bench.py's practical_peak comes from the newest committed membw probe,
+    the 4:1 pattern over every variant of it (profiles/r05_membw.json)."""
+    import bench
+    pc = bench.practical_ceiling("read4to1")
+    assert pc is not None and "r05_membw.json" in pc[1]
+    import json
+    d = json.load(open(os.path.join(ROOT, "profiles", "r05_membw.json")))
+    best = max(v[1] for k, v in d.items() if k.startswith(("read4to1", "r4w")))
+    assert pc[0] == best and best > 6000
+    cp = bench.practical_ceiling("copy")
+    assert cp is not None and cp[0] > 6000
