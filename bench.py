@@ -301,17 +301,40 @@ def _launcher_selftest(args, world, rank, local):
 # elapsed time, its stage means (HIP events, vsig_timing) and the exposed
 # waits of its exchanges (StreamChain.enable_wait_timing), all-gathered.
 RANK_FIELDS = ("ms_per_step", "fir", "psd", "xcorr", "refine", "left_halo_wait",
-               "right_halo_wait", "gather_wait")
+               "right_halo_wait", "gather_wait", "fir_ghz", "psd_ghz", "xcorr_ghz")
+CLOCK_STAGES = ("fir", "psd", "xcorr")
 
 
-def rank_row(elapsed, steps, stages, waits):
-    """One rank's diagnostics in ms (per step; a stage or wait it lacks is 0)."""
+def rank_row(elapsed, steps, stages, waits, clocks=None):
+    """One rank's diagnostics in ms (per step; a stage or wait it lacks is 0)
+    and its stages' effective clocks in GHz (0 if not measured)."""
     row = {"ms_per_step": elapsed / steps * 1e3}
     for k in ("fir", "psd", "xcorr", "refine"):
         row[k] = float(stages.get(k, 0.0))
     for k in ("left_halo", "right_halo", "gather"):
         row[k + "_wait"] = float(waits.get(k, 0.0))
+    for k in CLOCK_STAGES:
+        row[k + "_ghz"] = float((clocks or {}).get(k, 0.0))
     return row
+
+
+def stage_clocks(lib, h, run, nsteps):
+    """Effective clock of each stage (GHz) over `nsteps` untimed steps `run()`
+    with the library's clock sinks on (vsig_clock_*: the shader clock against
+    the 100 MHz real-time counter over every 64th block's lifetime)."""
+    import ctypes as C
+    if lib.vsig_clock_enable(h, 1) != 0:
+        return {}
+    for _ in range(nsteps):
+        run()
+    torch.cuda.synchronize()
+    out = {}
+    for name in CLOCK_STAGES + ("pfb",):
+        ghz, ticks = C.c_double(), C.c_int64()
+        if lib.vsig_clock_read(h, name.encode(), C.byref(ghz), C.byref(ticks)) == 0 and ticks.value:
+            out[name] = round(ghz.value, 3)
+    lib.vsig_clock_enable(h, 0)
+    return out
 
 
 def gather_rank_rows(row, world, dev):
@@ -375,7 +398,6 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
     lib, h = be.ctx.lib, be.ctx.h
     lib.vsig_timing_reset(h)
     lib.vsig_timing_enable(h, 0 if args.no_kernel_timing else 1)
-    chain.enable_wait_timing(world > 1 and not args.no_kernel_timing)
     torch.cuda.synchronize()
     barrier()
     t0 = time.perf_counter()
@@ -395,13 +417,26 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
         lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
         if cnt.value:
             stages[name] = tot.value / cnt.value
+    # untimed diagnostic steps after the timed loop (the timed steps stay the
+    # single-rank path's): each stage's effective clock, and at world > 1 the
+    # exposed waits of the exchanges
+    clocks, waits = {}, {}
+    ndiag = 0 if args.no_kernel_timing else 3
+    if ndiag:
+        clocks = stage_clocks(lib, h, chain.step, ndiag)
+        if world > 1:
+            chain.enable_wait_timing(True)
+            for _ in range(ndiag):
+                chain.step()
+            torch.cuda.synchronize()
+            waits = chain.wait_ms(ndiag)
+            chain.enable_wait_timing(False)
+        barrier()
     ranks = None
     if world > 1:
-        # every rank's own clock, stage means and exposed waits, gathered so the
-        # line says which rank and which exchange set the pace
-        waits = chain.wait_ms(steps)
-        chain.enable_wait_timing(False)
-        rows = gather_rank_rows(rank_row(elapsed, steps, stages, waits), world, dev)
+        # every rank's own elapsed time, stage means, clocks and exposed waits,
+        # gathered so the line says which rank and which exchange set the pace
+        rows = gather_rank_rows(rank_row(elapsed, steps, stages, waits, clocks), world, dev)
         ranks = summarize_ranks(rows)
         elapsed = max(r["ms_per_step"] for r in rows) * steps * 1e-3
     ny = n // decim
@@ -481,8 +516,11 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
                            "GBs_per_gpu": round(chain_bytes / (ms_per_step * 1e-3) / 1e9, 1),
                            "hbm_frac": round(chain_bytes / (ms_per_step * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                            "bytes_basis": f"{chain_bytes / n:.2f} B/input sample"}
+    for k, g in clocks.items():
+        if k in stage_roof:
+            stage_roof[k]["ghz"] = g
     return {"elapsed": elapsed, "stages": stages, "stage_roof": stage_roof, "roof": roof,
-            "check": check, "taps": taps, "tmpl": tmpl, "ranks": ranks}
+            "check": check, "taps": taps, "tmpl": tmpl, "ranks": ranks, "clocks": clocks}
 
 
 def main():
@@ -614,6 +652,7 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},
+        "stages_ghz": leg["clocks"],
         "stages_roofline": stage_roof,
         "stages_roofline_c2": stages_c2,
         "check": check,
@@ -661,6 +700,7 @@ def run_sync(args, world, rank, local, dev):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     lib.vsig_timing_enable(h, 0)
+    clocks = {} if args.no_kernel_timing else stage_clocks(lib, h, lambda: xc(x, "valid", peak=pk), 3)
     peak, idx, s1, s2 = dsp._read_peak(pk)
     nout = n - L + 1
     conf = dsp._confidence(peak, s1, s2, nout, 0.5)
@@ -687,6 +727,8 @@ def run_sync(args, world, rank, local, dev):
         stage = {"xcorr": {"ms": round(ms, 4), "TFLOPs": round(tf, 2),
                            "valu_peak_TFLOPs": FP32_PEAK_TF, "valu_frac": round(tf / FP32_PEAK_TF, 4),
                            "M": M}}
+        if "xcorr" in clocks:
+            stage["xcorr"]["ghz"] = clocks["xcorr"]
     cpu = None
     if not args.no_cpu_baseline:
         from oracle import ref        # the CPU baseline leg only
@@ -755,6 +797,8 @@ def run_pfb(args, world, rank, local, dev):
     t1 = time.perf_counter()
     barrier()
     lib.vsig_timing_enable(h, 0)
+    clocks = {} if args.no_kernel_timing else stage_clocks(lib, h, ch.step, 3)
+    barrier()
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -785,6 +829,8 @@ def run_pfb(args, world, rank, local, dev):
                 "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
                 "algorithmic_bytes": nbytes, "avg_launch_ms": round(ms, 4),
                 "traffic_source": pmc["source"] if pmc else None}
+        if "pfb" in clocks:
+            roof["ghz"] = clocks["pfb"]
     cpu = None
     if world == 1 and not args.no_cpu_baseline:
         from oracle import ref        # the CPU baseline leg only

@@ -147,6 +147,14 @@ const char* vsig_build_id(void);
 int vsig_timing_enable(vsig_ctx* ctx, int on);
 int vsig_timing_read(vsig_ctx* ctx, const char* kernel, double* total_ms, int64_t* launches);
 int vsig_timing_reset(vsig_ctx* ctx);
+/* Per-stage effective clock (a diagnostic, for bench.py's untimed clock steps):
+ * while enabled (enable zeroes the sums), the FIR, PSD, correlator and PFB
+ * kernels sample the shader clock and the 100 MHz real-time counter at the
+ * start and end of every 64th block (wave 0); read returns the mean clock in
+ * GHz of a kernel family over those blocks' lifetimes (0 if none ran) and the
+ * real-time ticks it averaged over. */
+int vsig_clock_enable(vsig_ctx* ctx, int on);
+int vsig_clock_read(vsig_ctx* ctx, const char* kernel, double* ghz, int64_t* ticks);
 
 /* ---- spectrum: Sxx[f, k] = |sum_{i<nperseg} w[i] x[f*hop + i] e^{-2 pi j k i / nfft}|^2 * scale
  * nfft: any length >= nperseg up to 2^27 (powers of two in [64, 2^28]: in-LDS plans, above

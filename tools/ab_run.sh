@@ -8,5 +8,5 @@ mkdir -p gpurun_out
 for lib in "$@"; do
   if [ "$lib" = base ]; then unset VSIG_LIB; else export VSIG_LIB=$GRAFT_REPO_ROOT/vector_amd/$lib.so; fi
   timeout -k 10 240 python3 bench.py $ARGS --no-cpu-baseline > gpurun_out/${TAG}_$lib.json 2> gpurun_out/${TAG}_$lib.err
-  python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_$lib.json')); print('$lib', d['ms_per_step'], d.get('stages_ms'), d['check']['ok'])"
+  python3 -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_$lib.json')); print('$lib', d['ms_per_step'], d.get('stages_ms'), d.get('stages_ghz'), d['check']['ok'])"
 done

@@ -138,11 +138,48 @@ __device__ __forceinline__ float2 twc(float2 b) {
 }
 
 // One radix-2 Stockham step inside registers: Ns = 2^P.  The step runs in
-// three phases over all its butterflies J -- (A) the first half of every
-// twiddle product, (B) the second half, (C) the sums -- so that a packed op
-// and its consumer are never adjacent: gfx950 needs one wait state between a
-// packed fp32 op and a dependent one, and hipcc pads every inline-asm
-// boundary with one, while independent work in between costs nothing.
+// two phases over all its butterflies J -- (A) each twiddled operand's
+// ratio form u, (C) the sums -- so that a packed op and its consumer are never
+// adjacent: gfx950 needs one wait state between a packed fp32 op and a
+// dependent one, and hipcc pads every inline-asm boundary with one, while
+// independent work in between costs nothing.
+// General twiddles w = c - i s take the ratio (Linzer-Feig) form: with
+// rot(b) = (b.y, -b.x), w b = c (b + (s/c) rot(b)) when |c| >= |s|, else
+// s ((c/s) b + rot(b)) -- u is one packed fma with the swizzle and the sign in
+// op_sel / neg_hi, and x0 +- w b two packed fmas with the scalar (c or s):
+// 3 packed ops per butterfly instead of 4 (a product in two halves, then an
+// add and a sub).  The ratio is at most 1, so the rounding is the product's.
+template <int K, int M>
+struct RatioTw {
+  static constexpr int idx = K * (64 / M);
+  static constexpr float c = kCos64[idx], s = kSin64[idx];
+  static constexpr bool cbig = (c < 0 ? -c : c) >= (s < 0 ? -s : s);
+  static constexpr float ratio = cbig ? (float)((double)s / (double)c) : (float)((double)c / (double)s);
+  static constexpr float scale = cbig ? c : s;
+};
+template <int K, int M>
+__device__ __forceinline__ float2 ratio_u(float2 b) {
+  using T = RatioTw<K, M>;
+  const f2v bv = tov(b), rr = (f2v){T::ratio, T::ratio};
+  f2v r;
+  if constexpr (T::cbig)      // b + ratio * (b.y, -b.x)
+    asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
+        : "=v"(r) : "v"(bv), "s"(rr));
+  else                        // ratio * b + (b.y, -b.x)
+    asm("v_pk_fma_f32 %0, %1, %2, %1 op_sel:[0,0,1] op_sel_hi:[1,1,0] neg_hi:[0,0,1]"
+        : "=v"(r) : "v"(bv), "s"(rr));
+  return fromv(r);
+}
+// a - h * u with a compile-time scalar h (the same SGPR pair as cfma_s, negated
+// by the neg modifiers)
+__device__ __forceinline__ float2 cfms_s(float2 u, float h, float2 a) {
+  f2v r;
+  const f2v hh = (f2v){h, h};
+  asm("v_pk_fma_f32 %0, %1, %2, %3 neg_lo:[0,1,0] neg_hi:[0,1,0]"
+      : "=v"(r) : "v"(tov(u)), "s"(hh), "v"(tov(a)));
+  return fromv(r);
+}
+
 template <int R, int P>
 struct Radix2Phased {
   static constexpr int Ns = 1 << P, M = 2 * Ns;
@@ -153,31 +190,17 @@ struct Radix2Phased {
   }
   __device__ __forceinline__ static void run(const float2* a, float2* t) {
     float2 u[R / 2];
-    // (A) general twiddles: b * cos; 45-degree family: (b.x +- b.y, ...)
+    // (A) general twiddles: the ratio form; 45-degree family: (b.x +- b.y, ...)
     static_for<0, R / 2>([&](auto ji) {
       constexpr int J = decltype(ji)::value;
       constexpr int k = kk<J>();
       const float2 b = a[J + R / 2];
       if constexpr (general<J>()) {
-        constexpr int idx = k * (64 / M);
-        u[J] = fromv(tov(b) * (f2v){kCos64[idx], kCos64[idx]});
+        u[J] = ratio_u<k, M>(b);
       } else if constexpr (8 * k == M) {
         u[J] = cadd_mi(b, b);
       } else if constexpr (8 * k == 3 * M) {
         u[J] = csub_mi(b, b);
-      }
-    });
-    // (B) general twiddles: + sin * (b.y, -b.x)
-    static_for<0, R / 2>([&](auto ji) {
-      constexpr int J = decltype(ji)::value;
-      if constexpr (general<J>()) {
-        constexpr int idx = kk<J>() * (64 / M);
-        const float2 b = a[J + R / 2];
-        const f2v bv = tov(b), ss = (f2v){kSin64[idx], kSin64[idx]};
-        f2v r;
-        asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[0,1,1] neg_hi:[1,0,0]"
-            : "=v"(r) : "v"(bv), "s"(ss), "v"(tov(u[J])));
-        u[J] = fromv(r);
       }
     });
     // (C) the butterflies' sums
@@ -196,50 +219,17 @@ struct Radix2Phased {
       } else if constexpr (8 * k == M) {           // h (b.x + b.y, b.y - b.x)
         constexpr float h = 7.071067812e-01f;
         t[o] = cfma_s(u[J], h, x0);
-        t[o + Ns] = cfma_s(u[J], -h, x0);
+        t[o + Ns] = cfms_s(u[J], h, x0);
       } else if constexpr (8 * k == 3 * M) {       // -h (b.x - b.y, b.x + b.y)
         constexpr float h = 7.071067812e-01f;
-        t[o] = cfma_s(u[J], -h, x0);
+        t[o] = cfms_s(u[J], h, x0);
         t[o + Ns] = cfma_s(u[J], h, x0);
       } else {
-        t[o] = cadd(x0, u[J]);
-        t[o + Ns] = csub(x0, u[J]);
+        constexpr float sc = RatioTw<k, M>::scale;
+        t[o] = cfma_s(u[J], sc, x0);
+        t[o + Ns] = cfms_s(u[J], sc, x0);
       }
     });
-  }
-};
-
-template <int R, int P, int J>
-struct Radix2Step {
-  __device__ __forceinline__ static void run(const float2* a, float2* t) {
-    constexpr int Ns = 1 << P;
-    constexpr int k = J & (Ns - 1);
-    constexpr int o = ((J >> P) << (P + 1)) + k;
-    const float2 x0 = a[J];
-    const float2 b = a[J + R / 2];
-    constexpr int M = 2 * Ns;
-    if constexpr (k == 0) {
-      t[o] = cadd(x0, b);
-      t[o + Ns] = csub(x0, b);
-    } else if constexpr (4 * k == M) {           // (-i) b folded into the adds
-      t[o] = cadd_mi(x0, b);
-      t[o + Ns] = csub_mi(x0, b);
-    } else if constexpr (8 * k == M) {           // h (b.x + b.y, b.y - b.x)
-      constexpr float h = 7.071067812e-01f;
-      const float2 u = cadd_mi(b, b);
-      t[o] = cfma_s(u, h, x0);
-      t[o + Ns] = cfma_s(u, -h, x0);
-    } else if constexpr (8 * k == 3 * M) {       // -h (b.x - b.y, b.x + b.y)
-      constexpr float h = 7.071067812e-01f;
-      const float2 u = csub_mi(b, b);
-      t[o] = cfma_s(u, -h, x0);
-      t[o + Ns] = cfma_s(u, h, x0);
-    } else {
-      const float2 x1 = twc<k, M>(b);
-      t[o] = cadd(x0, x1);
-      t[o + Ns] = csub(x0, x1);
-    }
-    if constexpr (J + 1 < R / 2) Radix2Step<R, P, J + 1>::run(a, t);
   }
 };
 
@@ -952,10 +942,15 @@ struct xpad<Plan1024x, 2> {
 };
 // The correlator's / PSD's 8192-point plan with conflict-free exchanges (Swz).
 using Plan8192x = Swz<Plan8192>;
-// The same size on 512 threads x 16 values (four passes, the radix-2 one with
-// a single exact twiddle per thread): half the VGPRs of Plan8192x, so two
-// 512-thread correlator blocks per CU run four waves per SIMD.
-using Plan8192w = Swz<Plan<8192, 16, 16, 2, 16, 16>>;
+// The correlator's 8192-point halves: radices 32 / 8 / 32.  Against 16 / 32 /
+// 16 the middle pass's four radix-8 butterflies per thread share one k (TF a
+// multiple of Ns = 32), so its twiddles come from one anchor (6 generated
+// powers per transform instead of 27) and the last pass's 31 from four
+// (27 instead of 2 x 13); the register DFTs cost the same.  The identity map
+// keeps the radix-32 first pass's stores conflict-free (16-lane groups write
+// 33 j + r: distinct banks for 16 consecutive j; the sigma map's even j would
+// meet 2-way) and its segment loads 512-byte runs per wave.
+using Plan8192c = Lanes<Plan<8192, 32, 32, 8, 32>, kMapId, kMapId, 5>;
 // The PSD's 8192-point plan with interleaved first / last passes (16-byte
 // frame loads, 8-byte |X|^2 stores, conflict-free exchanges).
 using Plan8192i = Lanes<Plan8192, kMapIlv, kMapIlv, 5, 1>;

@@ -80,10 +80,11 @@ template <class P, bool MIX = false, bool X4 = false, bool XS = false>
 __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ Hs,
     int lo, long long hop, int decim, float2* __restrict__ y, long long nblocks,
-    const float2* __restrict__ tw, MixArgs mix) {
+    const float2* __restrict__ tw, MixArgs mix, unsigned long long* clk) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   __shared__ float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
+  const ClockStamp cs(clk, blockIdx.x);
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (2 * b >= nblocks) return;  // uniform per block
   const long long nloc = n - g0;
@@ -117,6 +118,7 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
     fir_store<P>(a, y, b0, hop, lo, nloc, decim, t);
     fir_store<P>(d, y, b1, hop, lo, nloc, decim, t);
   }
+  cs.done(clk);
 }
 
 // ---------------------------------------------------------------------------
@@ -227,7 +229,7 @@ template <bool MIX = false, bool X4 = false>
 __global__ __launch_bounds__(64) void fir_poly_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
     long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
-    const float2* __restrict__ twd, MixArgs mix) {
+    const float2* __restrict__ twd, MixArgs mix, unsigned long long* clk) {
   using P = Plan1024q;
   using PD = Plan256d;
   constexpr int D = 4;
@@ -236,6 +238,7 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
   static_assert(lds_need<PD>() <= lds_size<P>(), "exchange buffer");
   __shared__ float2 lds[lds_size<P>()];
   const int t0 = threadIdx.x;
+  const ClockStamp cs(clk, blockIdx.x);
   const long long nloc = n - g0;
   const int tq0 = (t0 & 15) | ((t0 & 16) << 1) | ((t0 & 32) >> 1);
   float2 wa[nanch_total<P>()];
@@ -291,6 +294,7 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
       if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, cconj(u[e]));
     }
   }
+  cs.done(clk);
 }
 
 // G_k[j] (see fir_poly_kernel) from Hs = FFT_1024(h) / 1024, in double.
@@ -331,12 +335,14 @@ hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const flo
   const dim3 g((unsigned)((nblocks + 1) / 2)), blk(64);
   const MixArgs m = mix ? *mix : MixArgs{};
   if (mix)
-    hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+    hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m,
+                       g_clock_sink);
   else if (x4_aligned(x, g0 - lo2, hop))
     hipLaunchKernelGGL((fir_poly_kernel<false, true>), g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw,
-                       twd, m);
+                       twd, m, g_clock_sink);
   else
-    hipLaunchKernelGGL(fir_poly_kernel<false>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m);
+    hipLaunchKernelGGL(fir_poly_kernel<false>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m,
+                       g_clock_sink);
   return hipGetLastError();
 }
 
@@ -375,7 +381,7 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
     if constexpr (PL::TF == 64) {
       if (mix) {
         hipLaunchKernelGGL((fir_os_kernel<PL, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps - 1,
-                           hop, decim, y, nblocks, tw, m);
+                           hop, decim, y, nblocks, tw, m, g_clock_sink);
         return;
       }
     }
@@ -394,15 +400,15 @@ hipError_t launch_fir_os(int M, const float2* x, long long n, long long g0, cons
       if (x4_aligned(x, g0 - lo, hop)) {
         if (xs)
           hipLaunchKernelGGL((fir_os_kernel<PL, false, true, true>), grid, dim3(PL::TF), 0, st, x, n, g0,
-                             Hs, lo, hop, decim, y, nblocks, tw, m);
+                             Hs, lo, hop, decim, y, nblocks, tw, m, g_clock_sink);
         else
           hipLaunchKernelGGL((fir_os_kernel<PL, false, true>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs,
-                             lo, hop, decim, y, nblocks, tw, m);
+                             lo, hop, decim, y, nblocks, tw, m, g_clock_sink);
         return;
       }
     }
     hipLaunchKernelGGL((fir_os_kernel<PL, false>), grid, dim3(PL::TF), 0, st, x, n, g0, Hs, ntaps - 1,
-                       hop, decim, y, nblocks, tw, m);
+                       hop, decim, y, nblocks, tw, m, g_clock_sink);
   };
   switch (M) {
     case 1024: run(Plan1024x{}); break;

@@ -42,7 +42,9 @@ template <class PL, int PT, int VAR>
 __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float2* __restrict__ x, long long n,
                                                   const float* __restrict__ h, long long M,
                                                   long long fpg, float2* __restrict__ y,
-                                                  const float2* __restrict__ tw) {
+                                                  const float2* __restrict__ tw,
+                                                  unsigned long long* clk) {
+  const ClockStamp cs(clk, blockIdx.x);
   constexpr int C = PL::N, E = PL::E, TF = PL::TF, G = 256 / C;
   constexpr int U = PT / cgcd(E, PT);          // batches per ring period
   static_assert(G * E * TF == 256, "one FFT thread per (frame, t) of a batch");
@@ -138,6 +140,7 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
     if (inside) walk(IC<0>{}, IC<0>{});
     else walk(IC<0>{}, IC<1>{});
   }
+  cs.done(clk);
 }
 
 // Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3;
@@ -157,7 +160,7 @@ static void launch_pfb_t(const float2* x, long long n, const float* h, long long
   const long long groups = (M + fpg - 1) / fpg;
   const long long blocks = (groups + G - 1) / G;
   hipLaunchKernelGGL((pfb_kernel<PL, PT, PL::N == 64 ? kPfbVar64 : 3>), dim3((unsigned)blocks), dim3(256), 0, st, x, n, h, M,
-                     fpg, y, tw);
+                     fpg, y, tw, g_clock_sink);
 }
 
 hipError_t launch_pfb(int C, int PT, const float2* x, long long n, const float* h, long long M,

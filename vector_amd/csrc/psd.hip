@@ -31,10 +31,11 @@ template <class P>
 __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
     const float2* __restrict__ x, long long stride, const float* __restrict__ win, int nperseg,
     long long hop, float scale, float* __restrict__ out, long long nframes, int shift,
-    const float2* __restrict__ tw, bool x4) {
+    const float2* __restrict__ tw, bool x4, unsigned long long* clk) {
   static_assert(P::TF >= 256, "one frame per block");
   __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
+  const ClockStamp cs(clk, blockIdx.x);
   const long long u = blockIdx.x;
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
@@ -108,6 +109,7 @@ __global__ __launch_bounds__(P::TF) void psd_pair_kernel(
       }
     }
   }
+  cs.done(clk);
 }
 
 // Smaller plans (several frames per 256-thread block): two-level twiddle
@@ -279,13 +281,15 @@ hipError_t launch_psd(int N, const float2* x, long long stride, const float* win
     const bool x4 = stride == 1 && nperseg == N && hop % 2 == 0 &&
                     (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(win) & 7) == 0;
     hipLaunchKernelGGL(psd_pair_kernel<Plan8192i>, dim3((unsigned)((nframes + 1) / 2)), dim3(Plan8192i::TF),
-                       0, st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, x4);
+                       0, st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, x4,
+                       g_clock_sink);
     return hipGetLastError();
   }
   VSIG_PLAN_SWITCH(N, {
     if constexpr (PL::TF >= 256) {
       hipLaunchKernelGGL(psd_pair_kernel<PL>, dim3((unsigned)((nframes + 1) / 2)), dim3(PL::TF), 0,
-                         st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, false);
+                         st, x, stride, win, nperseg, hop, scale, out, nframes, shift, tw, false,
+                         g_clock_sink);
     } else {
       constexpr int FPB = block_threads<PL>() / PL::TF;
       hipLaunchKernelGGL(psd_split_kernel<PL>, dim3((unsigned)((nframes + FPB - 1) / FPB)),
@@ -332,9 +336,9 @@ hipError_t plan_info(int N, int* radices, int* npasses) {
     for (int q = 0; q < Plan1024s::NP; ++q) radices[q] = Plan1024s::R[q];
     return hipSuccess;
   }
-  if (N == -8192) {                 // the 512-thread 8192-point plan (correlator halves)
-    *npasses = Plan8192w::NP;
-    for (int q = 0; q < Plan8192w::NP; ++q) radices[q] = Plan8192w::R[q];
+  if (N == -8192) {                 // the correlator halves' 8192-point plan
+    *npasses = Plan8192c::NP;
+    for (int q = 0; q < Plan8192c::NP; ++q) radices[q] = Plan8192c::R[q];
     return hipSuccess;
   }
   if (N == -16384) {                // the 512-thread plan (M = 32768 correlator halves)

@@ -18,6 +18,11 @@ struct TimingRec {
 };
 
 constexpr size_t kRefineKeysBytes = 64;   // refine.hip RefineKeys (the scratch header)
+constexpr int kClockSlots = 32;            // per-stage clock sinks (vsig_clock_*)
+
+namespace vsig {
+thread_local unsigned long long* g_clock_sink = nullptr;
+}
 
 struct vsig_ctx {
   int device = 0;
@@ -54,6 +59,9 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
+  bool clock = false;                    // per-stage clock sinks on (vsig_clock_enable)
+  unsigned long long* clkbuf = nullptr;  // kClockSlots x {shader ticks, 100 MHz ticks}
+  std::map<std::string, int> clkslot;
 };
 
 struct vsig_fir {
@@ -196,17 +204,27 @@ int ensure_stage(vsig_ctx* c, int i, size_t bytes) {
   return VSIG_OK;
 }
 
-// Event pair around one kernel launch (only when timing is on).
+// Event pair around one kernel launch (only when timing is on); with the
+// clock option on, the stage's clock sink for the launches in its scope.
 struct Timed {
   vsig_ctx* c;
   hipEvent_t b = nullptr, e = nullptr;
   const char* name;
-  Timed(vsig_ctx* c_, const char* n) : c(c_), name(n) {
+  unsigned long long* prev_sink;
+  Timed(vsig_ctx* c_, const char* n) : c(c_), name(n), prev_sink(vsig::g_clock_sink) {
+    if (c->clock && c->clkbuf) {
+      auto it = c->clkslot.find(name);
+      int slot = -1;
+      if (it != c->clkslot.end()) slot = it->second;
+      else if ((int)c->clkslot.size() < kClockSlots) slot = c->clkslot[name] = (int)c->clkslot.size();
+      if (slot >= 0) vsig::g_clock_sink = c->clkbuf + 2 * slot;
+    }
     if (!c->timing) return;
     if (hipEventCreate(&b) != hipSuccess || hipEventCreate(&e) != hipSuccess) { b = e = nullptr; return; }
     (void)hipEventRecord(b, c->stream);
   }
   ~Timed() {
+    vsig::g_clock_sink = prev_sink;
     if (!b) return;
     (void)hipEventRecord(e, c->stream);
     c->timers[name].ev.emplace_back(b, e);
@@ -539,6 +557,7 @@ void vsig_free(vsig_ctx* c) {
   for (auto& kv : c->chirps) { (void)hipFree(kv.second.c); (void)hipFree(kv.second.B); }
   if (c->bigtmp) (void)hipFree(c->bigtmp);
   for (int i = 0; i < 2; ++i) if (c->spec[i]) (void)hipFree(c->spec[i]);
+  if (c->clkbuf) (void)hipFree(c->clkbuf);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -644,6 +663,30 @@ int vsig_copy_dev(vsig_ctx* c, void* dst, const void* src, int64_t bytes) {
 int vsig_synchronize(vsig_ctx* c) {
   if (!c) return VSIG_E_INVALID;
   HIPCHK(c, hipStreamSynchronize(c->stream));
+  return VSIG_OK;
+}
+
+int vsig_clock_enable(vsig_ctx* c, int on) {
+  if (!c) return VSIG_E_INVALID;
+  if (on) {
+    if (!c->clkbuf) HIPCHK(c, hipMalloc(&c->clkbuf, 2 * kClockSlots * sizeof(unsigned long long)));
+    HIPCHK(c, hipMemsetAsync(c->clkbuf, 0, 2 * kClockSlots * sizeof(unsigned long long), c->stream));
+  }
+  c->clock = on != 0;
+  return VSIG_OK;
+}
+
+int vsig_clock_read(vsig_ctx* c, const char* kernel, double* ghz, int64_t* ticks) {
+  if (!c || !kernel || !ghz) return VSIG_E_INVALID;
+  *ghz = 0.0;
+  if (ticks) *ticks = 0;
+  auto it = c->clkslot.find(kernel);
+  if (!c->clkbuf || it == c->clkslot.end()) return VSIG_OK;
+  unsigned long long h[2] = {0, 0};
+  HIPCHK(c, hipStreamSynchronize(c->stream));
+  HIPCHK(c, hipMemcpy(h, c->clkbuf + 2 * it->second, sizeof(h), hipMemcpyDeviceToHost));
+  if (h[1]) *ghz = (double)h[0] / (double)h[1] * 0.1;      // s_memrealtime runs at 100 MHz
+  if (ticks) *ticks = (int64_t)h[1];
   return VSIG_OK;
 }
 

@@ -16,6 +16,40 @@ __device__ __forceinline__ long long xcd_remap(long long b, long long nb) {
   return x * q + (x < r ? x : r) + i;
 }
 
+// Per-stage effective clock (vsig_clock_*, a diagnostic the bench runs in
+// untimed steps after its timed loop).  When a launch gets a sink, wave 0 of
+// every 64th block reads the shader clock (s_memtime) and the 100 MHz
+// real-time counter (s_memrealtime) at its start and at its end and adds both
+// differences into sink[0] / sink[1] by vector atomics; the clock over the
+// sampled blocks' lifetimes is then sink[0] / sink[1] x 100 MHz.  With no sink
+// (the default) nothing is read and nothing is written.
+struct ClockStamp {
+  unsigned long long t0 = 0, r0 = 0;
+  bool on;
+  __device__ __forceinline__ ClockStamp(unsigned long long* sink, unsigned long long blk)
+      : on(sink != nullptr && (blk & 63) == 0) {
+    if (on) {
+      t0 = __builtin_amdgcn_s_memtime();
+      r0 = __builtin_amdgcn_s_memrealtime();
+      // lgkmcnt(0) alone: the counters' returns are retired here, so the
+      // compiler's waits for the kernel's LDS reads stay counted (an SMEM read
+      // left pending on one path makes every later LDS wait a full drain)
+      __builtin_amdgcn_s_waitcnt(0xC07F);
+    }
+  }
+  __device__ __forceinline__ void done(unsigned long long* sink) const {
+    if (on && threadIdx.x < 2) {
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      const unsigned long long r1 = __builtin_amdgcn_s_memrealtime();
+      atomicAdd(sink + threadIdx.x, threadIdx.x == 0 ? t1 - t0 : r1 - r0);
+    }
+  }
+};
+// The sink of the launch being issued on this host thread (set by the C-ABI
+// layer's per-stage timer when the clock option is on, else null); the launch
+// functions pass it to the kernels that take one.
+extern thread_local unsigned long long* g_clock_sink;
+
 enum { VSIG_C128 = 0, VSIG_C64 = 1, VSIG_F64 = 2, VSIG_F32 = 3 };
 
 // NCO mixer of apply_frequency_shift (utils.py:120-127): x[gi] * exp(j theta),

@@ -120,16 +120,21 @@ __global__ __launch_bounds__(P::TF) void xcorr_os_kernel(
 // ---------------------------------------------------------------------------
 // The M = 32768 correlator (templates of 8193 .. 16384 samples in one pass):
 // 16384-point halves, 512 threads x 32 values, 3 passes, one block per CU.
-// Measured on templates of 4096 (round 2): 1.89 ms per 2^28 samples against
-// 1.42 ms for the M = 16384 kernel (r02_v6 A/B), so shorter templates keep
-// M = 16384.
+// Measured on templates of 4096: 1.89 ms per 2^28 samples against 1.42 ms for
+// the M = 16384 kernel (round 2, r02_v6 A/B), and again on round 6's kernels
+// 2.65-2.68 against 2.24-2.25 ms at config 5 (profiles/r06_xcorr_plan_ab.txt:
+// one 512-thread block per CU has no second block to run while its waves meet
+// at the exchange barriers), so shorter templates keep M = 16384.
 using PlanX32k = Plan16384w;
-// The sigma map (conflict-free exchanges, 8-byte loads).  Measured against
-// it (round 2-3): the interleaved map (16-byte loads, two split twiddles per
+// The 32 / 8 / 32 identity-map plan (Plan8192c, fft_engine.hpp); round 6:
+// 2.24-2.25 ms at config 5 against 2.27-2.28 for round 5's 16 / 32 / 16 sigma
+// map (profiles/r06_xcorr_plan_ab.txt).  Measured against the sigma map
+// (rounds 2-3): the interleaved map (16-byte loads, two split twiddles per
 // thread) 2.67 vs 2.58 ms at config 5 (profiles/r02_v19_ab.txt); the
-// 512-thread, 16-value Plan8192w (4 waves per SIMD, a third exchange per half)
-// 2.67 vs 2.48 ms (r03_v11).
-using PlanX16k = Plan8192x;
+// 512-thread, 16-value plan (4 waves per SIMD, a third exchange per half)
+// 2.67 vs 2.48 ms (r03_v11), +11 % in round 5.
+using PlanX16k = Plan8192c;
+constexpr int kPlanKey16k = -8192;      // its twiddle table (plan_info)
 
 // in_index(t, e) = base(t) + off(e): the split twiddle
 // W_M^in_index = W_M^base * W_64^half_root(e).
@@ -355,7 +360,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     const float2* __restrict__ s, long long n, const float4* __restrict__ Ps2, long long off,
     long long nout, long long hop, float2* __restrict__ c, int store_mode,
     PeakPartial* __restrict__ partials, long long nblocks, const float2* __restrict__ tw,
-    const float2* __restrict__ wt, unsigned* __restrict__ lkeys) {
+    const float2* __restrict__ wt, unsigned* __restrict__ lkeys, unsigned long long* clk) {
   static_assert(P::R[0] == P::RL, "overlap-save needs a palindromic plan");
   static_assert(map0_of<P>::value != kMapIlv, "one split twiddle per thread");
   constexpr int M = 2 * P::N;
@@ -363,6 +368,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
                 "per-element split twiddles must be 64th roots of unity");
   __shared__ __attribute__((aligned(16))) float2 lds[lds_size<P>()];
   const int t = threadIdx.x;
+  const ClockStamp cs(clk, blockIdx.x);
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
@@ -418,6 +424,7 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
 #pragma unroll
   for (int k = 0; k < kPfLines; ++k)   // the prefetch loads stay; their values are never used
     asm volatile("" ::"v"(pfv[k]));
+  cs.done(clk);
 }
 
 hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps, long long off,
@@ -437,18 +444,18 @@ hipError_t launch_xcorr_os(int M, const float2* s, long long n, const float2* Ps
     if (dv) {
       hipLaunchKernelGGL((xcorr_half_kernel<PlanX16k, kDv>), dim3((unsigned)nblocks),
                          dim3(PlanX16k::TF), 0, st, s, n, reinterpret_cast<const float4*>(Ps), off, nout,
-                         hop, c, store_mode, partials, nblocks, tw, wt, lkeys);
+                         hop, c, store_mode, partials, nblocks, tw, wt, lkeys, g_clock_sink);
       return hipGetLastError();
     }
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX16k>, dim3((unsigned)nblocks), dim3(PlanX16k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt, lkeys);
+                       partials, nblocks, tw, wt, lkeys, g_clock_sink);
     return hipGetLastError();
   }
   if (M == 32768) {     // 16384-point halves, one block per CU
     hipLaunchKernelGGL(xcorr_half_kernel<PlanX32k>, dim3((unsigned)nblocks), dim3(PlanX32k::TF), 0,
                        st, s, n, reinterpret_cast<const float4*>(Ps), off, nout, hop, c, store_mode,
-                       partials, nblocks, tw, wt, lkeys);
+                       partials, nblocks, tw, wt, lkeys, g_clock_sink);
     return hipGetLastError();
   }
   auto run = [&](auto plan) {
@@ -487,7 +494,7 @@ hipError_t xcorr_geom(int M, int* waves, int* Q, int* stride, int* plan, int* ws
   *rsub = 1;
   if (M == 32768) { *waves = PlanX32k::TF / 64; *Q = 2 * PlanX32k::E; *stride = PlanX32k::TF; *plan = -16384; }
   else if (M == 16384) {
-    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::TF; *plan = 8192;
+    *waves = PlanX16k::TF / 64; *Q = 2 * PlanX16k::E; *stride = PlanX16k::TF; *plan = kPlanKey16k;
   }
   else if (M == 8192) { *waves = Plan8192::TF / 64; *Q = Plan8192::E; *stride = Plan8192::TF; *plan = 8192; }
   else if (M == 4096) { *waves = Plan4096::TF / 64; *Q = Plan4096::E; *stride = Plan4096::TF; *plan = 4096; }
