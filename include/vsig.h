@@ -321,7 +321,9 @@ int vsig_abs_c128_dev(vsig_ctx* ctx, int32_t dtype, const void* a, int64_t n, vo
  * vector_amd/shard.py StreamChain; reference precedent: the
  * overlapped chunking of heavy_packet_optimizer.py:114-152).  Rank r of world
  * owns input samples [r n, (r+1) n) of one capture; per step: left halo
- * (ntaps-1 input samples from rank r-1) -> FIR + decimate -> right halo (L-1
+ * (hist = ntaps-1 input samples rounded up to a multiple of 16, so that the
+ * FIR's segments start on 128-byte lines: the last hist samples of rank r-1;
+ * world > 1 needs n >= hist) -> FIR + decimate -> right halo (L-1
  * filtered samples from rank r+1) -> PSD (nfft, hop nfft) -> valid
  * correlation with the template + exact peak -> all-gather of the 32-byte
  * peak records.  Results equal one chain over the whole capture.

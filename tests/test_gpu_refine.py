@@ -488,6 +488,54 @@ def test_watchdog_fire_is_an_error_and_recovers(gpu):
     assert nat.global_peak()[1] == ref_lag
 
 
+def test_watchdog_fire_survives_scratch_growth(gpu):
+    """a fire in a device-tensor Correlator pass whose
+    status nobody read lives in the refine scratch's sticky fault word; when
+    the next, larger correlation grows that scratch the fault is carried into
+    the new one, so vsig_refine_status still reports 3 ('fired in some pass
+    since the last call'), and the pass after the report is clean and exact.
+    Runs on a fresh thread: its own context, so the scratch starts small."""
+    import threading
+    L, k1 = 4096, 5_000_011
+    pre = ref.qpsk_preamble(L, seed=5)
+    small = ref.synth_iq(1 << 20, seed=6)
+    big = ref.synth_iq(1 << 23, seed=7)
+    big[k1:k1 + L] += pre
+    res = {}
+
+    def body():
+        try:
+            xc = gpu.dsp.Correlator(pre)            # this thread's own context
+            ctx = xc.ctx
+
+            def wd(us):
+                ctx.check(ctx.lib.vsig_set_option(ctx.h, b"refine_watchdog_us", int(us)), "wd")
+            ds, db = torch.from_numpy(small).cuda(), torch.from_numpy(big).cuda()
+            wd(1)
+            try:
+                xc(ds, "valid")                     # fires; nothing reads the status here
+                torch.cuda.synchronize()
+            finally:
+                wd(2_000_000)
+            xc(db, "valid")                          # 8x the partials: a larger scratch
+            torch.cuda.synchronize()
+            res["after_growth"] = gpu.dsp.refine_status(ctx)[0]
+            _, pk = xc(db, "valid")
+            res["peak"] = gpu.dsp._read_peak(pk)
+            res["clean"] = gpu.dsp.refine_status(ctx)[0]
+        except BaseException as e:                   # re-raised in the test's thread
+            res["err"] = e
+
+    th = threading.Thread(target=body)
+    th.start()
+    th.join()
+    if "err" in res:
+        raise res["err"]
+    assert res["after_growth"] == 3
+    assert res["clean"] == 0
+    assert res["peak"][1] == k1
+
+
 @pytest.mark.parametrize("snr_db", [60, 40, 30, 20, 10, 0])
 def test_tone_under_noise_confidence(gpu, snr_db):
     """A tone template over a tone under complex noise: |c| has a high mean and

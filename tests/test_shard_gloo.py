@@ -209,6 +209,21 @@ def test_chain_config_validation():
         ChainConfig(n_local=128, taps=np.ones(3), nfft=64, template=np.ones(500)).validate(2)
 
 
+def test_chain_config_fir_halo_boundary():
+    """the left halo is ntaps-1 rounded up to 16 (128-byte-aligned
+    segment starts), so at world > 1 a chunk must hold that many samples --
+    the same bound as chain.hip's vsig_chain_create (ntaps-1 <= n_local < hist
+    made the send slice x_ext[n:n+hist] overlap the receive buffer x_ext[:hist])."""
+    from vector_amd.shard import ChainConfig, fir_history
+    assert fir_history(255) == 256 and fir_history(63) == 64 and fir_history(17) == 16
+    assert fir_history(1) == 0 and fir_history(18) == 32
+    taps = np.ones(40)                                  # ntaps - 1 = 39 -> hist 48
+    ChainConfig(n_local=48, taps=taps, nfft=8).validate(2)
+    ChainConfig(n_local=40, taps=taps, nfft=8).validate(1)       # one rank: no halo
+    with pytest.raises(ValueError, match="FIR halo"):   # n >= ntaps - 1 but < hist
+        ChainConfig(n_local=40, taps=taps, nfft=8).validate(2)
+
+
 # ---------------------------------------------------------------- sharded PFB (config 4)
 class OraclePfbBackend:
     """CPU stand-in for HipPfbBackend (test infrastructure)."""

@@ -88,6 +88,35 @@ __device__ __forceinline__ float2 cmul_cs(float2 b, float c, float s_) {
   return fromv(r);
 }
 __device__ __forceinline__ float2 cconj(float2 a) { return make_float2(a.x, -a.y); }
+// The conjugates of the overlap-save kernels (inverse transform by conj) with
+// the sign in the VOP3P neg modifiers -- the compiler's own form of a lone
+// conj negates both halves and moves one back (two instructions and a wait
+// state), and it does not fold one into a neighbouring asm product:
+// conj(v) as (v.x + 0, -v.y + 0)
+__device__ __forceinline__ float2 conj1(float2 v) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, 0 neg_hi:[1,0]" : "=v"(r) : "v"(tov(v)));
+  return fromv(r);
+}
+// conj(a * b): cmul with the high half's sum negated (neg_hi on its product
+// and its addend)
+__device__ __forceinline__ float2 cmul_conj(float2 a, float2 b) {
+  const f2v av = tov(a), bv = tov(b);
+  const f2v t = av * bv.xx;
+  f2v r;
+  asm("v_pk_fma_f32 %0, %1, %2, %3 op_sel:[1,1,0] op_sel_hi:[0,1,1] neg_lo:[1,0,0] neg_hi:[1,0,1]"
+      : "=v"(r) : "v"(av), "v"(bv), "v"(t));
+  return fromv(r);
+}
+// conj(a + b)
+__device__ __forceinline__ float2 cadd_conj(float2 a, float2 b) {
+  f2v r;
+  asm("v_pk_add_f32 %0, %1, %2 neg_hi:[1,1]" : "=v"(r) : "v"(tov(a)), "v"(tov(b)));
+  return fromv(r);
+}
+// (The correlator's spectrum product conj(X) P keeps cmul(cconj(a), b): the
+// same as two asm ops it measured 1.3 % slower at config 5 -- the asm pair took
+// the kernel from 206 to 253 VGPRs, profiles/r06_conj_std_ab.txt.)
 
 // cos / sin of 2*pi*k/64, k = 0..31 (enough for every in-register radix <= 64).
 constexpr float kCos64[32] = {

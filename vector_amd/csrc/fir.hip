@@ -17,7 +17,7 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
 #pragma unroll
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e) - lo;
-      if (i >= 0 && i < lim) st_stream(yb + (unsigned)i, cconj(v[e]));
+      if (i >= 0 && i < lim) st_stream(yb + (unsigned)i, conj1(v[e]));
     }
   } else {
     // i / decim by a multiply-high with m = floor(2^32 / decim) + 1: exact for
@@ -28,7 +28,7 @@ __device__ __forceinline__ void fir_store(const float2* v, float2* __restrict__ 
     for (int e = 0; e < P::E; ++e) {
       const int i = out_index<P>(t, e) - lo;
       const unsigned q = __umulhi((unsigned)i, mg);
-      if (i >= 0 && i < lim && (unsigned)i == q * (unsigned)decim) st_stream(yb + q, cconj(v[e]));
+      if (i >= 0 && i < lim && (unsigned)i == q * (unsigned)decim) st_stream(yb + q, conj1(v[e]));
     }
   }
 }
@@ -49,7 +49,7 @@ __device__ __forceinline__ void fir_store_x4(const float2* v, float2* __restrict
   float2* yb = y + gb;
 #pragma unroll
   for (int i = 0; i < P::E / 2; ++i) {
-    const float2 p = cconj(v[2 * i]), q = cconj(v[2 * i + 1]);
+    const float2 p = conj1(v[2 * i]), q = conj1(v[2 * i + 1]);
     const auto rx = __builtin_amdgcn_permlane32_swap(__float_as_uint(p.x), __float_as_uint(q.x), false, false);
     const auto ry = __builtin_amdgcn_permlane32_swap(__float_as_uint(p.y), __float_as_uint(q.y), false, false);
     const int io = 2 * t + 128 * i - lo;               // even: lo is
@@ -106,8 +106,8 @@ __global__ __launch_bounds__(P::TF) void fir_os_kernel(
 #pragma unroll
   for (int e = 0; e < P::E; ++e) {
     const float2 h = Hs[out_index<P>(t, e)];
-    a[e] = cconj(cmul(a[e], h));
-    d[e] = cconj(cmul(d[e], h));
+    a[e] = cmul_conj(a[e], h);
+    d[e] = cmul_conj(d[e], h);
   }
   launder_anchors<P>(wa);
   fft_pair<P>(a, d, lds, TwAnchors{wa}, t);
@@ -211,13 +211,14 @@ __device__ __forceinline__ float2 swap32_add(float2 a, float2 b) {
   return cadd(make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0])),
               make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
 }
-// the same across (l, l ^ 16): lanes with bit 4 clear return a(l) + a(l + 16),
-// the others b(l - 16) + b(l).
-__device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
+// the same across (l, l ^ 16), conjugated (the inverse transform's operand):
+// lanes with bit 4 clear return conj(a(l) + a(l + 16)), the others
+// conj(b(l - 16) + b(l)).
+__device__ __forceinline__ float2 swap16_add_conj(float2 a, float2 b) {
   const auto rx = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.x), __float_as_uint(b.x), false, false);
   const auto ry = __builtin_amdgcn_permlane16_swap(__float_as_uint(a.y), __float_as_uint(b.y), false, false);
-  return cadd(make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0])),
-              make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
+  return cadd_conj(make_float2(__uint_as_float(rx[0]), __uint_as_float(ry[0])),
+                   make_float2(__uint_as_float(rx[1]), __uint_as_float(ry[1])));
 }
 
 // A memory-only knock-out of this kernel (both transform pairs skipped,
@@ -225,7 +226,14 @@ __device__ __forceinline__ float2 swap16_add(float2 a, float2 b) {
 // for the kernel then (profiles/r02_v12_ab.txt), i.e. the loads / stores of
 // this access pattern alone run at 5.5 TB/s and the transforms add ~0.45 ms.
 
-template <bool MIX = false, bool X4 = false>
+// STD: the chain's geometry (255 taps: lo2 = 256, hop = 768), for which every
+// thread's stored outputs are known at compile time -- circular indices
+// i = tq + 64 e, kept for n0 = 64 <= i < n1 = 256, i.e. e = 1..3 on every lane
+// -- so a pair whose outputs all lie inside the chunk stores with no
+// per-element compare or exec-mask branch (the last pair keeps the tests).
+constexpr int kStdLo2 = 256, kStdHop = 768;
+
+template <bool MIX = false, bool X4 = false, bool STD = false>
 __global__ __launch_bounds__(64) void fir_poly_kernel(
     const float2* __restrict__ x, long long n, long long g0, const float2* __restrict__ G, int lo2,
     long long hop, float2* __restrict__ y, long long nblocks, const float2* __restrict__ tw,
@@ -277,10 +285,26 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
     }
     const float2 sa0 = swap32_add(pa[0], pa[1]), sa1 = swap32_add(pa[2], pa[3]);
     const float2 sd0 = swap32_add(pd[0], pd[1]), sd1 = swap32_add(pd[2], pd[3]);
-    ua[i] = cconj(swap16_add(sa0, sa1));
-    ud[i] = cconj(swap16_add(sd0, sd1));
+    ua[i] = swap16_add_conj(sa0, sa1);
+    ud[i] = swap16_add_conj(sd0, sd1);
   }
   fft_pair<PD>(ua, ud, lds, TwRegs{wr}, tq);
+  if constexpr (STD) {
+    static_assert(out_off<PD>(1) == 64 && PD::E == 4 && kStdLo2 / D == 64 &&
+                  (kStdLo2 + kStdHop) / D == 256, "e = 1..3 kept on every lane");
+    // both segments' last output (index 255) inside the chunk: uniform
+    if ((2 * b + 1) * kStdHop - kStdLo2 + 255LL * D < nloc) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        float2* yb = y + (2 * b + f) * (kStdHop / D) - kStdLo2 / D + tq;
+        const float2* u = f ? ud : ua;
+#pragma unroll
+        for (int e = 1; e < PD::E; ++e) st_stream(yb + 64 * e, conj1(u[e]));
+      }
+      cs.done(clk);
+      return;
+    }
+  }
   const int n0 = lo2 / D, n1 = (lo2 + (int)hop) / D;
 #pragma unroll
   for (int f = 0; f < 2; ++f) {
@@ -291,7 +315,7 @@ __global__ __launch_bounds__(64) void fir_poly_kernel(
 #pragma unroll
     for (int e = 0; e < PD::E; ++e) {
       const int i = out_index<PD>(tq, e);
-      if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, cconj(u[e]));
+      if (i >= n0 && i < n1 && gb + (long long)i * D < nloc) st_stream(yb + i, conj1(u[e]));
     }
   }
   cs.done(clk);
@@ -337,6 +361,9 @@ hipError_t launch_fir_poly(const float2* x, long long n, long long g0, const flo
   if (mix)
     hipLaunchKernelGGL(fir_poly_kernel<true>, g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw, twd, m,
                        g_clock_sink);
+  else if (x4_aligned(x, g0 - lo2, hop) && lo2 == kStdLo2 && hop == kStdHop)
+    hipLaunchKernelGGL((fir_poly_kernel<false, true, true>), g, blk, 0, st, x, n, g0, G, lo2, hop, y,
+                       nblocks, tw, twd, m, g_clock_sink);
   else if (x4_aligned(x, g0 - lo2, hop))
     hipLaunchKernelGGL((fir_poly_kernel<false, true>), g, blk, 0, st, x, n, g0, G, lo2, hop, y, nblocks, tw,
                        twd, m, g_clock_sink);

@@ -338,11 +338,31 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
   r.wd_ticks = (unsigned long long)c->refine_wd_us * 100ull;   // s_memrealtime: 100 MHz
   const size_t need = vsig::refine_scratch_bytes(r);
   const bool fresh = need > c->rscratch_bytes;
+  // a watchdog fire of an earlier pass whose status nobody read (device-tensor
+  // callers) lives in the old scratch's sticky fault word: carry it into the
+  // new one, so vsig_refine_status still reports 3 ("fired in some pass since
+  // the last call"), and clear the fused launch's counters as that report
+  // does (a fire can leave them inconsistent)
+  unsigned long long pending_fault = 0;
+  if (fresh && c->rscratch) {
+    unsigned long long keys[6];      // refine.hip RefineKeys: ..., fault
+    HIPCHK(c, hipMemcpyAsync(keys, c->rscratch, sizeof(keys), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    pending_fault = keys[5];
+  }
   int rc = ensure_buf(c, &c->rscratch, &c->rscratch_bytes, need);
   if (rc) return rc;
   // a new scratch starts with zero keys (the sticky fault word is read by
   // vsig_refine_status; the finalize resets only the per-launch words)
   if (fresh) HIPCHK(c, hipMemsetAsync(c->rscratch, 0, kRefineKeysBytes, c->stream));
+  if (pending_fault) {
+    HIPCHK(c, hipMemcpyAsync(static_cast<unsigned long long*>(c->rscratch) + 5, &pending_fault,
+                             sizeof(pending_fault), hipMemcpyHostToDevice, c->stream));
+    if (c->partials)
+      HIPCHK(c, hipMemsetAsync(c->partials + c->npartials + vsig::kFinalizeTmp, 0,
+                               vsig::kCounterRecs * sizeof(PeakPartial), c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));     // pending_fault is a host local
+  }
   r.scratch = c->rscratch;
   r.rec = rec;
   r.out128 = out128;

@@ -58,8 +58,19 @@ class ChainConfig:
             raise ValueError("n_local/decim must be a multiple of nfft (frames never straddle chunks)")
         if self.template is not None and world > 1 and ny < len(self.template) - 1:
             raise ValueError("chunk shorter than the template halo")
-        if world > 1 and self.n_local < len(self.taps) - 1:
-            raise ValueError("chunk shorter than the FIR halo")
+        # the left halo is ntaps-1 samples rounded up to 16 (StreamChain.hist:
+        # 128-byte-aligned segment starts); a shorter chunk would make the send
+        # slice x_ext[n:n+hist] overlap the receive buffer x_ext[:hist] of one
+        # sendrecv (chain.hip's vsig_chain_create rejects the same configs)
+        if world > 1 and self.n_local < fir_history(len(self.taps)):
+            raise ValueError("chunk shorter than the FIR halo "
+                             f"(n_local {self.n_local} < {fir_history(len(self.taps))})")
+
+
+def fir_history(ntaps: int) -> int:
+    """Left-halo length of a time chunk: ntaps - 1 input samples rounded up to a
+    multiple of 16 (so [halo | chunk]'s FIR segments start on 128-byte lines)."""
+    return (ntaps - 1 + 15) // 16 * 16
 
 
 def combine_peaks(rows: np.ndarray) -> tuple[float, int, float, float]:
@@ -200,7 +211,7 @@ class StreamChain:
         # that [halo | chunk] puts the FIR's segment starts on 128-byte lines
         # (D = 4: lo2 = 256 at 255 taps; the surplus samples are never read by
         # a tap; profiles/r05_fir_align_ab.txt)
-        self.hist = (len(cfg.taps) - 1 + 15) // 16 * 16
+        self.hist = fir_history(len(cfg.taps))
         self.ny = cfg.n_local // cfg.decim
         self.L = len(cfg.template) if cfg.template is not None else 0
         self.yhalo = (self.L - 1) if (self.L and rank < world - 1) else 0
