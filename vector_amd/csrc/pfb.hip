@@ -38,6 +38,12 @@ __device__ __forceinline__ f2v tap_fma(f2v hp, f2v u, f2v a) {
 // and stores, so their HBM latency overlaps the compute (more bytes in flight
 // per CU for the same occupancy).
 // VAR bit 2: cap registers for 4 waves / SIMD (4 blocks per CU).
+//
+// Measured against (round 6, profiles/r06_pfb_ab.txt): each group's wave
+// transforming its own 8 frames (wave barriers only, LDS padding 1 per 8,
+// frames 72 float2 apart) 1.596-1.599 ms against 1.537-1.543 for this
+// block-wide layout with its five barriers per batch.
+
 template <class PL, int PT, int VAR>
 __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float2* __restrict__ x, long long n,
                                                   const float* __restrict__ h, long long M,
@@ -48,8 +54,18 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
   constexpr int C = PL::N, E = PL::E, TF = PL::TF, G = 256 / C;
   constexpr int U = PT / cgcd(E, PT);          // batches per ring period
   static_assert(G * E * TF == 256, "one FFT thread per (frame, t) of a batch");
-  __shared__ float2 lds[G * E * PL::LDS];
+  // frame slots of a batch: FB = G E frames, each in an LDS slice of S float2
+  // (odd: see the FFT role below)
+  constexpr int FB = G * E, S = PL::LDS | 1;
+  __shared__ float2 lds[FB * S];
   const int tid = threadIdx.x, p = tid % C, g = tid / C;
+  // the FFT's twiddle table (56 .. 240 entries) copied into LDS once: no
+  // global loads inside a batch -- a table load there waits, by vmcnt's issue
+  // order, for the next batch's row prefetch as well -- and no VGPRs (exact
+  // register twiddles push the 4-wave C = 64 kernel into spills); the 16 lanes
+  // of an access group read one entry (broadcast)
+  __shared__ float2 twl[PL::twsize()];
+  for (int i = tid; i < PL::twsize(); i += 256) twl[i] = tw[i];
   // taps in pairs (h[2j C + p], h[(2j + 1) C + p]): one packed FMA per tap
   // with the pair's low / high half broadcast through op_sel
   static_assert(PT % 2 == 0, "tap pairs");
@@ -72,17 +88,34 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
     }
   };
   constexpr bool PF = (VAR & 2) != 0;
-  // FFT role of this thread: frame slot ff of the batch, thread t of the frame
-  const int ff = tid / TF, t = tid % TF;
-  float2* fl = lds + ff * PL::LDS;
+  // FFT role of this thread: frame slot ff of the batch, thread t of the frame,
+  // frames across the lanes (ff = tid mod FB): the 16 lanes of an LDS access
+  // group then hold 16 frames at one intra-frame index, at addresses S apart,
+  // and an odd S puts them on 16 distinct banks for every exchange of the
+  // engine (with ff = tid / TF two frames' threads met 2-4 way)
+  const int ff = tid % FB, t = tid / FB;
+  float2* fl = lds + ff * S;
   // Odd groups walk their frames backwards: the PT - 1 rows two neighbouring
-  // groups share are then read by both at the same time (both walks start, or
-  // both end, there), so the second read is an L2 hit instead of a re-fetch
-  // from HBM one whole walk later.  Walk step f is frame mf(f); its new row is
-  // the frame's last row (forward) or first row (backward); ring slot of row
-  // mf(f) + q: (f + q) % PT forward, (f + PT - 1 - q) % PT backward.
-  auto walk = [&](auto bwdc, auto chkc) {
+  // groups share are then read by both near the same time (both walks start,
+  // or both end, there), so the second read is an L2 hit instead of a
+  // re-fetch from HBM one whole walk later.  Walk step f is frame mf(f); its
+  // new row is the frame's last row (forward) or first row (backward); ring
+  // slot of row mf(f) + q: (f + q) % PT forward, (f + PT - 1 - q) % PT backward.
+  // Where two groups of a block END at their shared rows (even group g
+  // forward, g + 1 backward) the walks meet those rows in opposite orders, up
+  // to PT - 2 steps apart -- long enough for L2 to lose many of them (round 6
+  // PMC: 1.18 x algorithmic reads).  With XCH (PT = 2 E, two batches per ring
+  // period, the whole block inside the stream) the pair shares them through
+  // LDS instead: in the second-to-last batch each group also stores its new
+  // rows 1 .. E-1 to its slot of xb, and in the last batch each takes its new
+  // rows 1 .. E-1 from the partner's slot (row E - i of it: the partner met
+  // them in the opposite order) -- 14 of the 15 shared rows read from HBM once.
+  // The last batch issues no prefetch (its rows lie past the walk).
+  constexpr bool XCH_OK = PF && PT == 2 * E && U == 2 && G % 2 == 0;
+  __shared__ float2 xb[XCH_OK ? G * (E - 1) * C : 1];
+  auto walk = [&](auto bwdc, auto chkc, auto xchc) {
     constexpr bool BWD = decltype(bwdc)::value;
+    constexpr bool X = XCH_OK && decltype(xchc)::value;
     auto rf = [&](long long f) { return BWD ? fpg - 1 - f : f; };     // frame offset
     auto mf = [&](long long f) { return m0 + rf(f); };
     auto newrow = [&](long long f) { return BWD ? rf(f) : rf(f) + PT - 1; };
@@ -96,29 +129,49 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
       for (int i = 0; i < E; ++i) nxt[i] = row(newrow(i), chkc);
     }
     for (long long b = 0; b < fpg; b += (long long)E * U) {
+      const bool last = b + (long long)E * U >= fpg;           // uniform
       static_for<0, U>([&](auto ui) {
         constexpr int u = decltype(ui)::value;
         static_for<0, E>([&](auto ii) {
           constexpr int i = decltype(ii)::value;
           constexpr int k = u * E + i;                        // walk step mod ring period
-          if constexpr (PF) ring[(k + PT - 1) % PT] = nxt[i];
-          else ring[(k + PT - 1) % PT] = row(newrow(b + k), chkc);
+          if constexpr (X && u == U - 1 && i >= 1) {
+            if (last) ring[(k + PT - 1) % PT] = xb[((g ^ 1) * (E - 1) + (E - i) - 1) * C + p];
+            else ring[(k + PT - 1) % PT] = nxt[i];
+          } else if constexpr (PF) {
+            ring[(k + PT - 1) % PT] = nxt[i];
+          } else {
+            ring[(k + PT - 1) % PT] = row(newrow(b + k), chkc);
+          }
           f2v z[2] = {(f2v){0.f, 0.f}, (f2v){0.f, 0.f}};   // even / odd taps: no
           static_for<0, PT>([&](auto qi) {                    // back-to-back dependence
             constexpr int q = decltype(qi)::value;
             constexpr int slot = BWD ? (k + PT - 1 - q) % PT : (k + q) % PT;
             z[q & 1] = tap_fma<q & 1>(hq2[q / 2], tov(ring[slot]), z[q & 1]);
           });
-          lds[(g * E + i) * PL::LDS + lpad(p)] = fromv(z[0] + z[1]);
+          lds[(g * E + i) * S + lpad(p)] = fromv(z[0] + z[1]);
         });
-        if constexpr (PF) {
+        if constexpr (X && u == 0) {
+          if (last) {
 #pragma unroll
-          for (int i = 0; i < E; ++i) nxt[i] = row(newrow(b + (u + 1) * E + i), chkc);   // next batch
+            for (int i = 1; i < E; ++i) xb[(g * (E - 1) + i - 1) * C + p] = nxt[i];
+          }
+        }
+        if constexpr (PF) {
+          if (!(last && u == U - 1)) {                        // next batch
+            if (X && u == 0 && last) {                        // only its row 0 from HBM
+              nxt[0] = row(newrow(b + (u + 1) * E), chkc);
+            } else {
+#pragma unroll
+              for (int i = 0; i < E; ++i) nxt[i] = row(newrow(b + (u + 1) * E + i), chkc);
+            }
+          }
         }
         __syncthreads();
         float2 v[E];
         fft_load<PL, 0>(v, fl, t);
-        fft_frame<PL>(v, fl, tw, t);
+        fft_stage<PL, 0>(v, TwTable{twl}, t);
+        fft_tail<PL, 1>(v, fl, TwTable{twl}, t);
         static_assert(VAR & 1, "the walk directions need the LDS-staged stores");
         __syncthreads();                                      // last FFT pass read lds
 #pragma unroll
@@ -127,25 +180,31 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
 #pragma unroll
         for (int i = 0; i < E; ++i) {
           const long long m = mf(b + u * E + i);
-          if (m < M) y[m * C + p] = lds[(g * E + i) * PL::LDS + lpad(p)];
+          if (m < M) y[m * C + p] = lds[(g * E + i) * S + lpad(p)];
         }
         __syncthreads();                                      // lds reused by the next batch
       });
     }
   };
+  // the exchange needs both groups of every pair on the unchecked path: the
+  // whole block inside the stream (block-uniform); other blocks check bounds
+  const bool inside_blk = (((blk + 1) * G) * fpg + PT - 1) * C <= n;
+  const bool fast = XCH_OK ? inside_blk : inside;
   if (gid & 1) {
-    if (inside) walk(IC<1>{}, IC<0>{});
-    else walk(IC<1>{}, IC<1>{});
+    if (fast) walk(IC<1>{}, IC<0>{}, IC<1>{});
+    else walk(IC<1>{}, IC<1>{}, IC<0>{});
   } else {
-    if (inside) walk(IC<0>{}, IC<0>{});
-    else walk(IC<0>{}, IC<1>{});
+    if (fast) walk(IC<0>{}, IC<0>{}, IC<1>{});
+    else walk(IC<0>{}, IC<1>{}, IC<0>{});
   }
   cs.done(clk);
 }
 
 // Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3;
-// C = 64: registers capped for 4 waves / SIMD, VAR 7), 64 frames per group
-// (128 / 256 / 512 measured slower, profiles/r02_v13_pfb_ab.txt).
+// C = 64: registers capped for 4 waves / SIMD, VAR 7: 128 VGPRs, no scratch),
+// 64 frames per group (128 / 256 / 512 measured slower, profiles/r02_v13_pfb_ab.txt;
+// again in round 6 with the row exchange: 128 +9 %, 32 +0.1..1 %; VAR 3 +1 %,
+// profiles/r06_pfb_ab.txt).
 constexpr int kPfbVar64 = 7;
 constexpr long long kPfbFramesPerGroup = 64;
 template <class PL, int PT>
