@@ -114,9 +114,10 @@ __device__ __forceinline__ float2 cadd_conj(float2 a, float2 b) {
   asm("v_pk_add_f32 %0, %1, %2 neg_hi:[1,1]" : "=v"(r) : "v"(tov(a)), "v"(tov(b)));
   return fromv(r);
 }
-// (The correlator's spectrum product conj(X) P keeps cmul(cconj(a), b): the
-// same as two asm ops it measured 1.3 % slower at config 5 -- the asm pair took
-// the kernel from 206 to 253 VGPRs, profiles/r06_conj_std_ab.txt.)
+// (The correlator's spectrum product conj(X) P keeps cmul(cconj(a), b): with
+// the conj folded into neg modifiers -- two asm ops, or cmul's own shape with
+// one -- it measured 1.3-4 % slower at config 5 (206 -> 249-253 VGPRs),
+// profiles/r06_conj_std_ab.txt.)
 
 // cos / sin of 2*pi*k/64, k = 0..31 (enough for every in-register radix <= 64).
 constexpr float kCos64[32] = {
@@ -483,6 +484,11 @@ __device__ __forceinline__ int opaque_zero() {
 //             retired in issue order).
 struct TwTable { const float2* tw; };
 struct TwAnchors { const float2* wa; };
+//  TwAnchorsX: anchors, except that a pass whose butterflies all share one k
+//             (one anchor set) and whose radix is at most 8 takes its R - 1
+//             exact twiddles from wx (load_twx: a few VGPRs, no generated
+//             powers; the correlator's radix-8 middle pass).
+struct TwAnchorsX { const float2* wa; const float2* wx; };
 //  TwLds    : a two-level table in LDS, W_N^m = A[m >> S] * B[m & (2^S - 1)]
 //             (S = ceil(log2 N / 2); <= 256 entries, 2 KB), filled once per
 //             block from global memory: LDS latency instead of an L2 round
@@ -535,6 +541,19 @@ __device__ __forceinline__ void load_rtw(float2* w, const float2* __restrict__ t
 
 template <class P>
 constexpr int nanch(int p) { return 1 + (P::R[p] - 1) / 8; }
+template <class P>
+constexpr int anch_nb(int p);
+// passes TwAnchorsX serves from exact register twiddles, and their offsets
+template <class P>
+constexpr bool twx_pass(int p) { return p >= 1 && p < P::NP && P::R[p] <= 8 && anch_nb<P>(p) == 1; }
+template <class P>
+constexpr int twx_off(int p) {
+  int o = 0;
+  for (int q = 1; q < p; ++q) o += twx_pass<P>(q) ? P::R[q] - 1 : 0;
+  return o;
+}
+template <class P>
+constexpr int twx_total() { return twx_off<P>(P::NP) > 0 ? twx_off<P>(P::NP) : 1; }
 // anchor sets per thread in pass p: one per butterfly, or a single one when
 // every butterfly j = m(t) + b TF of the thread has the same k = j mod Ns
 // (TF a multiple of Ns, maps other than kMapIlv)
@@ -552,6 +571,20 @@ constexpr int anch_off(int p) {
 }
 template <class P>
 constexpr int nanch_total() { return anch_off<P>(P::NP) > 0 ? anch_off<P>(P::NP) : 1; }
+
+// Load this thread's exact twiddles of the twx_pass passes (TwAnchorsX).
+template <class P>
+__device__ __forceinline__ void load_twx(float2* wx, const float2* __restrict__ tw, int t) {
+  static_for<1, P::NP>([&](auto pi) {
+    constexpr int p = decltype(pi)::value;
+    if constexpr (twx_pass<P>(p)) {
+      constexpr int R = P::R[p], Ns = P::ns(p);
+      const int k = bfly<P, p>(t, 0) & (Ns - 1);
+#pragma unroll
+      for (int r = 1; r < R; ++r) wx[twx_off<P>(p) + r - 1] = tw[P::twoff(p) + (r - 1) * Ns + k];
+    }
+  });
+}
 
 // Load this thread's anchors (thread t of its frame).
 template <class P>
@@ -592,6 +625,10 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
     const float2* wp = tws.w + rtw_off<P>(p) + (NB == 1 ? 0 : b) * (R - 1);
 #pragma unroll
     for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], wp[r - 1]);
+  } else if constexpr (std::is_same<TW, TwAnchorsX>::value && twx_pass<P>(p)) {
+    const float2* wp = tws.wx + twx_off<P>(p);
+#pragma unroll
+    for (int r = 1; r < R; ++r) v[b * R + r] = cmul(v[b * R + r], wp[r - 1]);
   } else if constexpr (std::is_same<TW, TwLds>::value) {
     constexpr int S = tw2_shift<P>();
     constexpr int stride = P::N / (Ns * R);       // W_{Ns R}^{rk} = W_N^{rk stride}
@@ -606,6 +643,8 @@ __device__ __forceinline__ void fft_twiddle(float2* v, TW tws, int t, int b) {
       v[b * R + r] = cmul(v[b * R + r], w);
     }
   } else {
+    static_assert(std::is_same<TW, TwAnchors>::value || std::is_same<TW, TwAnchorsX>::value,
+                  "twiddle source");
     constexpr int NA = nanch<P>(p);
     const float2* wa = tws.wa + anch_off<P>(p) + (anch_nb<P>(p) == 1 ? 0 : b) * NA;
     const float2 w1 = wa[0];

@@ -371,11 +371,16 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
   const ClockStamp cs(clk, blockIdx.x);
   float2 wa[nanch_total<P>()];
   load_anchors<P>(wa, tw, t);
+  // the radix-8 middle pass (one k per thread) from 7 exact twiddles in VGPRs
+  // instead of 6 generated powers per transform (TwAnchorsX): -0.5 % at
+  // config 5, profiles/r06_conj_std_ab.txt
+  float2 wx[twx_total<P>()];
+  load_twx<P>(wx, tw, t);
   const long long b = xcd_remap(blockIdx.x, gridDim.x);
   if (b >= nblocks) return;
   auto fft2 = [&](float2* x, float2* y) {
     launder_anchors<P>(wa);
-    fft_pair<P>(x, y, lds, TwAnchors{wa}, t);
+    fft_pair<P>(x, y, lds, TwAnchorsX{wa, wx}, t);
   };
   // W_M^base: base = in_index(t, 0), loaded ahead of the segment and the
   // prefetch below (loads complete in issue order)
@@ -399,6 +404,8 @@ __global__ __launch_bounds__(P::TF, xcorr_waves_per_eu<P>()) void xcorr_half_ker
     static_for<0, P::E>([&](auto ei) {
       constexpr int e = decltype(ei)::value;
       const float4 p = buf_load4(rp, v0, out_off<P>(e) * (int)sizeof(float4));
+      // (conj folded into the product's neg modifiers: fewer instructions,
+      // but +4 % at config 5 in both its forms, profiles/r06_conj_std_ab.txt)
       a[e] = cmul(cconj(a[e]), make_float2(p.x, p.y));
       d[e] = cmul(cconj(d[e]), make_float2(p.z, p.w));
     });
