@@ -352,7 +352,9 @@ constexpr int xcorr_waves_per_eu() { return P::E <= 16 ? 4 : P::TF >= 512 ? 1 : 
 // after the spectrum product the lines live long enough in the 4 MB L2 to be
 // evicted again (+45 % L2 fills).  Distances 32 / 96 / 128 / 192 / 256 are
 // slower or equal.  profiles/r03_v22_xcorr_segpf_ab.txt: -5 % correlator
-// time, +2.5 % reads.
+// time, +2.5 % reads.  Re-measured on round 6's 32 / 8 / 32 plan
+// (profiles/r06_xcorr_plan_ab.txt): 64 still best; 96 / 128 +1.7 / +2 %,
+// 48 +5 %, a prefetch of the block's own segment (no look-ahead) +6.7 %.
 constexpr int kSegPfDist = 64;
 
 template <class P, int DV = -1>
