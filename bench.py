@@ -377,7 +377,9 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
     cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=args.nfft, template=tmpl,
                       freq_shift=args.freq_shift, sample_rate=args.sample_rate)
     be = HipBackend(cfg, local)
-    chain = StreamChain(cfg, be, rank, world)
+    # the exact-argmax refine of step k beside step k + 1's FIR (its own stream,
+    # a second filtered-stream buffer; shard.StreamChain overlap_refine)
+    chain = StreamChain(cfg, be, rank, world, overlap_refine=not args.no_overlap_refine)
     N = world * n
     ny_total = N // decim
     k0 = (ny_total // 2 + 12_345) * decim     # global input sample of the preamble
@@ -446,6 +448,7 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
     check = {"sync_lag": lag, "expected": k0 // decim, "ok": bool(lag == k0 // decim)}
     ms_per_step = elapsed / steps * 1e3
     yhalo = chain.yhalo
+    overlapped = chain.overlap
     del chain, be
     torch.cuda.empty_cache()
 
@@ -499,7 +502,12 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
                                     "valu_peak_TFLOPs": FP32_PEAK_TF,
                                     "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
     if "refine" in stages:
-        stage_roof["refine"] = {"ms": round(stages["refine"], 4)}
+        # overlapped: the refine's own duration, beside the next step's FIR; the
+        # step's time beyond its three stages is what stays exposed (with the
+        # launch gaps between the stages)
+        stage_roof["refine"] = {"ms": round(stages["refine"], 4), "overlapped": overlapped,
+                                "step_minus_stages_ms": round(
+                                    ms_per_step - sum(stages.get(k, 0.0) for k in ("fir", "psd", "xcorr")), 4)}
     # north_star's FIR+FFT target on SURVEY.md §8(d)'s unfused byte count
     # (filter() writes y, spectrum() reads it): 8 + 8/D + 12/D B/sample
     if "fir" in stages and "psd" in stages:
@@ -545,6 +553,8 @@ def main():
                     help="processes for the all-cores CPU baseline (default: this process's CPU "
                          "allowance, bench.cpu_allowance, within host memory)")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--no-overlap-refine", action="store_true",
+                    help="run the refine on the step's stream (not beside the next step's FIR)")
     ap.add_argument("--no-refine", action="store_true",
                     help="skip the correlator's exact-argmax refine pass (A/B only)")
     ap.add_argument("--freq-shift", type=float, default=0.0,
@@ -648,7 +658,8 @@ def main():
                    "ntaps": args.ntaps, "decim": decim, "nfft": args.nfft,
                    "template": args.template,
                    "parallelism": f"time-chunk x{world} (RCCL halos)",
-                   "freq_shift": args.freq_shift, "refine": not args.no_refine},
+                   "freq_shift": args.freq_shift, "refine": not args.no_refine,
+                   "refine_overlapped": not (args.no_refine or args.no_overlap_refine)},
         "roofline": roof,
         "cpu_baseline": cpu,
         "stages_ms": {k: round(v, 4) for k, v in stages.items()},

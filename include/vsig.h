@@ -123,9 +123,27 @@ int vsig_synchronize(vsig_ctx* ctx);
  *                     record is left as the fp32 pass produced it and
  *                     vsig_refine_status reports status 1;
  *   "refine_watchdog_us" bound on the one-launch refine's two waits (default
- *                     2000000; a test hook: tiny values force a fire, status 3). */
+ *                     2000000; a test hook: tiny values force a fire, status 3);
+ *   "refine_async"    0 (default): the refine runs on the context stream after
+ *                     its correlator; 1: the refine of vsig_xcorr_exec_dev runs
+ *                     on the context's own refine stream (vsig_refine_stream),
+ *                     behind an event after the correlator, so the caller's next
+ *                     kernels (e.g. the next chunk's filter) overlap it.  The
+ *                     peak record is then complete only on the refine stream:
+ *                     read it after vsig_refine_join (the context stream waits
+ *                     for the last refine) or order its consumers on
+ *                     vsig_refine_stream; the caller must not overwrite the
+ *                     correlated stream before that.  The library itself joins
+ *                     before it reuses the refine's scratch (any later
+ *                     correlation, peak, statistics or staging call), and
+ *                     vsig_refine_status / vsig_synchronize wait for it. */
 int vsig_set_option(vsig_ctx* ctx, const char* key, int value);
 int vsig_get_option(const vsig_ctx* ctx, const char* key, int* value);
+/* The hipStream_t the "refine_async" refine runs on (the context stream when
+ * the option is off), and the join: the context stream waits for the last
+ * refine (an event; no host synchronisation). */
+void* vsig_refine_stream(vsig_ctx* ctx);
+int vsig_refine_join(vsig_ctx* ctx);
 /* Outcome of the context's last refine pass (synchronises the stream):
  * status 0 refined, 1 skipped (more candidate outputs than a refine_cap set
  * > 0), 2 no pass ran (refine off, or no correlation yet), 3 the one-launch

@@ -123,3 +123,49 @@ def test_stream_chain_long_template(gpu):
     i, rlag, peak, r1, r2, _ = ref.xcorr_peak(yr, tmpl, "valid")
     assert lag == rlag == k0
     _check_peak_on_own_stream(ch.y.cpu().numpy(), tmpl, m, lag, s1, s2)
+
+
+@pytest.mark.parametrize("decim", [4, 1])
+def test_overlapped_refine_back_to_back_steps(gpu, decim):
+    """bench.py's default step form (StreamChain overlap_refine): step k's
+    refine runs on the context's refine stream beside step k + 1's FIR, which
+    writes the other filtered-stream buffer.  Five steps back to back with the
+    preamble moved every step, the peak read only after the last one (and,
+    joined, after each of the first two): numpy's exact lag every time, the last
+    step's filtered stream and peak equal to the plain chain's, and a refine
+    fault check (status read) clean.  Then the plain path on the same context
+    (the option off again) is exact too."""
+    import torch
+    from vector_amd.shard import ChainConfig, HipBackend, StreamChain
+    n, L = 1 << 20, 4096 // decim
+    taps = scipy.signal.firwin(255, 0.2).astype(np.float32)
+    pre = ref.qpsk_preamble(L * decim, seed=41)
+    tmpl = np.convolve(pre, taps)[: L * decim][::decim].astype(np.complex64)
+    base = ref.synth_iq(n, seed=42)
+    k0s = [d * decim for d in (1000, 70_001, 123_457, 200_003, 33_333)]
+    xs = []
+    for k in k0s:
+        x = base.copy()
+        x[k: k + L * decim] += 3 * pre
+        xs.append(torch.from_numpy(x).cuda())
+    cfg = ChainConfig(n_local=n, taps=taps, decim=decim, nfft=8192 // decim, template=tmpl)
+    be = HipBackend(cfg, 0)
+    ch = StreamChain(cfg, be, 0, 1, overlap_refine=True)
+    assert ch.overlap and len(ch._y_bufs) == 2
+    for s, x in enumerate(xs):
+        ch.x.copy_(x)
+        ch.step()
+        if s < 2:
+            assert ch.global_peak()[1] == k0s[s] // decim
+    m, lag, s1, s2, nout = ch.global_peak()
+    assert lag == k0s[-1] // decim
+    be.check_refine()
+    y_last = ch.y.cpu().numpy()
+    plain = StreamChain(cfg, HipBackend(cfg, 0), 0, 1)
+    assert not plain.overlap
+    be.set_overlap_refine(False)
+    plain.x.copy_(xs[-1])
+    plain.step()
+    pm = plain.global_peak()
+    assert pm[1] == lag and pm[0] == m and pm[2] == s1 and pm[3] == s2
+    assert np.array_equal(plain.y.cpu().numpy(), y_last)

@@ -50,8 +50,13 @@ def _run_ranks(world, body):
     return res
 
 
-@pytest.mark.parametrize("world,decim", [(2, 4), (3, 4), (2, 1), (4, 4), (8, 4)])
-def test_stream_chain_hip_ranks(gpu, world, decim):
+@pytest.mark.parametrize("world,decim,overlap", [(2, 4, False), (3, 4, False), (2, 1, False),
+                                                 (4, 4, False), (8, 4, False), (2, 4, True),
+                                                 (3, 1, True), (4, 4, True)])
+def test_stream_chain_hip_ranks(gpu, world, decim, overlap):
+    """overlap: bench.py's default -- each rank's refine on its context's refine
+    stream beside its next step's FIR, two filtered-stream buffers, the peak
+    all-gather issued behind the refine (StreamChain overlap_refine)."""
     from vector_amd.shard import (ChainConfig, HipBackend, Loopback, NativeTransport,
                                   StreamChain)
     n, L, nfft = 1 << 19, 4096 // decim, 8192 // decim
@@ -85,7 +90,7 @@ def test_stream_chain_hip_ranks(gpu, world, decim):
 
     def body(r):
         ch = StreamChain(cfg(n), HipBackend(cfg(n), 0), r, world,
-                         transport=NativeTransport(lb.transport(r)))
+                         transport=NativeTransport(lb.transport(r)), overlap_refine=overlap)
         got = []
         for x in xs:
             ch.x.copy_(x[r * n:(r + 1) * n])

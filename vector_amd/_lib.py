@@ -75,6 +75,8 @@ SIGNATURES = {
     "vsig_timing_read": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(I64)]),
     "vsig_timing_reset": (C.c_int, [P]),
     "vsig_clock_enable": (C.c_int, [P, C.c_int]),
+    "vsig_refine_stream": (P, [P]),
+    "vsig_refine_join": (C.c_int, [P]),
     "vsig_clock_read": (C.c_int, [P, C.c_char_p, C.POINTER(C.c_double), C.POINTER(I64)]),
     "vsig_psd_c64_dev": (C.c_int, [P, P, I64, I64, P, I32, I64, I32, F32, I32, P, I64]),
     "vsig_psd_c64": (C.c_int, [P, P, I64, P, I32, I64, I32, F32, I32, P, I64]),

@@ -59,6 +59,15 @@ struct vsig_ctx {
   std::string err;
   bool timing = false;
   std::map<std::string, TimingRec> timers;
+  // "refine_async": the xcorr handle's refine on its own stream behind ev_corr,
+  // ev_ref recorded after it; joined (the context stream waits on ev_ref) before
+  // any reuse of its scratch -- see join_refine
+  int refine_async = 0;
+  hipStream_t rstream = nullptr;
+  hipEvent_t ev_corr = nullptr, ev_ref = nullptr;
+  bool refine_pending = false;           // an async refine was enqueued
+  bool refine_joined = false;            // ... and joined on refine_joined_on
+  hipStream_t refine_joined_on = nullptr;
   bool clock = false;                    // per-stage clock sinks on (vsig_clock_enable)
   unsigned long long* clkbuf = nullptr;  // kClockSlots x {shader ticks, 100 MHz ticks}
   std::map<std::string, int> clkslot;
@@ -97,6 +106,18 @@ namespace {
 int fail(vsig_ctx* c, int code, const std::string& msg) {
   if (c) c->err = msg;
   return code;
+}
+
+// The context stream waits for the last asynchronous refine (once per stream
+// after each refine): called before anything reuses the refine's scratch or
+// operands -- every scratch / partials / staging allocation and use below goes
+// through ensure_buf / ensure_partials / ensure_stage -- and by vsig_refine_join.
+void join_refine(vsig_ctx* c) {
+  if (!c->refine_pending) return;
+  if (c->refine_joined && c->refine_joined_on == c->stream) return;
+  (void)hipStreamWaitEvent(c->stream, c->ev_ref, 0);
+  c->refine_joined = true;
+  c->refine_joined_on = c->stream;
 }
 
 #define HIPCHK(ctx, expr)                                                              \
@@ -181,6 +202,7 @@ int get_half_tw(vsig_ctx* c, int M, int T, const float2** out) {
 }
 
 int ensure_partials(vsig_ctx* c, long long n) {
+  join_refine(c);
   if (n <= c->npartials) return VSIG_OK;
   if (c->partials) (void)hipFree(c->partials);
   c->partials = nullptr;
@@ -195,6 +217,7 @@ int ensure_partials(vsig_ctx* c, long long n) {
 }
 
 int ensure_stage(vsig_ctx* c, int i, size_t bytes) {
+  join_refine(c);
   if (bytes <= c->stage_bytes[i]) return VSIG_OK;
   if (c->stage[i]) (void)hipFree(c->stage[i]);
   c->stage[i] = nullptr;
@@ -211,7 +234,9 @@ struct Timed {
   hipEvent_t b = nullptr, e = nullptr;
   const char* name;
   unsigned long long* prev_sink;
-  Timed(vsig_ctx* c_, const char* n) : c(c_), name(n), prev_sink(vsig::g_clock_sink) {
+  hipStream_t st;
+  Timed(vsig_ctx* c_, const char* n, hipStream_t s = nullptr)
+      : c(c_), name(n), prev_sink(vsig::g_clock_sink), st(s ? s : c_->stream) {
     if (c->clock && c->clkbuf) {
       auto it = c->clkslot.find(name);
       int slot = -1;
@@ -221,12 +246,12 @@ struct Timed {
     }
     if (!c->timing) return;
     if (hipEventCreate(&b) != hipSuccess || hipEventCreate(&e) != hipSuccess) { b = e = nullptr; return; }
-    (void)hipEventRecord(b, c->stream);
+    (void)hipEventRecord(b, st);
   }
   ~Timed() {
     vsig::g_clock_sink = prev_sink;
     if (!b) return;
-    (void)hipEventRecord(e, c->stream);
+    (void)hipEventRecord(e, st);
     c->timers[name].ev.emplace_back(b, e);
   }
 };
@@ -254,6 +279,7 @@ int os_size_xcorr(long long L) {
 }
 
 int ensure_buf(vsig_ctx* c, void** buf, size_t* have, size_t bytes) {
+  join_refine(c);
   if (bytes <= *have) return VSIG_OK;
   if (*buf) (void)hipFree(*buf);
   *buf = nullptr;
@@ -307,7 +333,7 @@ struct RefineOperands {
 // launch finalizes them into rec and selects (thread columns when lkeys).
 int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, long long hop,
                long long nparts, int rev, const float2* c64, PeakPartial* rec, void* out128,
-               bool fused = false, const unsigned* lkeys = nullptr) {
+               bool fused = false, const unsigned* lkeys = nullptr, bool async = false) {
   c->refine_ran = false;
   if (!c->refine) return fused ? fail(c, VSIG_E_INVALID, "refine: fused finalize with refine off")
                              : VSIG_OK;
@@ -366,6 +392,20 @@ int run_refine(vsig_ctx* c, const RefineOperands& op, long long nout, int M, lon
   r.scratch = c->rscratch;
   r.rec = rec;
   r.out128 = out128;
+  if (async && c->refine_async) {
+    // on the refine stream behind the correlator; ev_ref marks its end
+    HIPCHK(c, hipEventRecord(c->ev_corr, c->stream));
+    HIPCHK(c, hipStreamWaitEvent(c->rstream, c->ev_corr, 0));
+    {
+      Timed t(c, "refine", c->rstream);
+      HIPCHK(c, vsig::launch_refine(r, c->rstream));
+    }
+    HIPCHK(c, hipEventRecord(c->ev_ref, c->rstream));
+    c->refine_pending = true;
+    c->refine_joined = false;
+    c->refine_ran = true;
+    return VSIG_OK;
+  }
   Timed t(c, "refine");
   HIPCHK(c, vsig::launch_refine(r, c->stream));
   c->refine_ran = true;
@@ -578,6 +618,9 @@ void vsig_free(vsig_ctx* c) {
   if (c->bigtmp) (void)hipFree(c->bigtmp);
   for (int i = 0; i < 2; ++i) if (c->spec[i]) (void)hipFree(c->spec[i]);
   if (c->clkbuf) (void)hipFree(c->clkbuf);
+  if (c->rstream) (void)hipStreamDestroy(c->rstream);
+  if (c->ev_corr) (void)hipEventDestroy(c->ev_corr);
+  if (c->ev_ref) (void)hipEventDestroy(c->ev_ref);
   if (c->own) (void)hipStreamDestroy(c->own);
   delete c;
 }
@@ -609,6 +652,14 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
   } else if (k == "blas_threads") {
     if (value < 1 || value > 1024) return fail(c, VSIG_E_INVALID, "blas_threads must be in [1, 1024]");
     c->blas_threads = value;
+  } else if (k == "refine_async") {
+    if (value && !c->rstream) {
+      HIPCHK(c, hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_corr, hipEventDisableTiming));
+      HIPCHK(c, hipEventCreateWithFlags(&c->ev_ref, hipEventDisableTiming));
+    }
+    if (!value) join_refine(c);
+    c->refine_async = value != 0;
   } else {
     return fail(c, VSIG_E_INVALID, "unknown option " + k);
   }
@@ -623,7 +674,19 @@ int vsig_get_option(const vsig_ctx* c, const char* key, int* value) {
   else if (k == "refine_cap") *value = (int)c->refine_cap;
   else if (k == "refine_watchdog_us") *value = (int)c->refine_wd_us;
   else if (k == "blas_threads") *value = c->blas_threads;
+  else if (k == "refine_async") *value = c->refine_async;
   else return VSIG_E_INVALID;
+  return VSIG_OK;
+}
+
+void* vsig_refine_stream(vsig_ctx* c) {
+  if (!c) return nullptr;
+  return (void*)(c->refine_async && c->rstream ? c->rstream : c->stream);
+}
+
+int vsig_refine_join(vsig_ctx* c) {
+  if (!c) return VSIG_E_INVALID;
+  join_refine(c);
   return VSIG_OK;
 }
 
@@ -631,6 +694,7 @@ int vsig_refine_status(vsig_ctx* c, int32_t* status, int64_t* candidates) {
   if (!c || !status || !candidates) return VSIG_E_INVALID;
   *status = 2;
   *candidates = 0;
+  join_refine(c);
   if (!c->refine_ran || !c->rscratch) return VSIG_OK;
   // refine.hip RefineKeys: count, lo_inv, hi_p1, status, done, fault
   unsigned long long keys[6];
@@ -682,6 +746,7 @@ int vsig_copy_dev(vsig_ctx* c, void* dst, const void* src, int64_t bytes) {
 
 int vsig_synchronize(vsig_ctx* c) {
   if (!c) return VSIG_E_INVALID;
+  join_refine(c);
   HIPCHK(c, hipStreamSynchronize(c->stream));
   return VSIG_OK;
 }
@@ -1019,7 +1084,7 @@ static void xcorr_release(vsig_xcorr* x) {
 // refine from the stored array.
 static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off, long long nout,
                      int store_mode, float2* cout, vsig_peak_t* peak_dev,
-                     const RefineOperands* op, void* out128) {
+                     const RefineOperands* op, void* out128, bool async = false) {
   vsig_ctx* c = x->ctx;
   PeakPartial* rec = peak_dev ? reinterpret_cast<PeakPartial*>(peak_dev) : c->result;
   if (x->Ps.size() == 1 && x->L <= (x->M == 32768 ? 16384 : 8192)) {
@@ -1059,7 +1124,7 @@ static int xcorr_run(vsig_xcorr* x, const float2* s, long long n, long long off,
     }
     if (out128 && cout) HIPCHK(c, vsig::launch_convert_c(1, cout, nout, out128, c->stream));
     return run_refine(c, *op, nout, x->M, hop, nparts, (store_mode & 4) ? 1 : 0, nullptr, rec, out128,
-                      fused, lk);
+                      fused, lk, async && peak_dev != nullptr);
   }
   constexpr long long B = 8192;
   constexpr int M = 16384;
@@ -1134,7 +1199,7 @@ int vsig_xcorr_exec_dev(vsig_xcorr* x, const void* s, int64_t n, int32_t mode, v
   // np.correlate(s, p): output o is full index (L - 1 - off) + o
   const RefineOperands op{s, n, x->tmpl, x->L, 0, (x->L - 1) - off};
   return xcorr_run(x, (const float2*)s, n, off, nout, cout ? 1 : 0, (float2*)cout, peak_dev, &op,
-                   nullptr);
+                   nullptr, true);
 }
 
 // np.correlate(a, v, mode): the shorter operand is the template; with

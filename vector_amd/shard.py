@@ -198,12 +198,35 @@ class HipBackend:
         check (the fault word is sticky on the device; synchronises)."""
         self.dsp.check_refine(self.ctx)
 
+    # -- the refine beside the next step (StreamChain overlap_refine) ---------
+    def set_overlap_refine(self, on: bool):
+        """The context's "refine_async" option (vsig.h): the correlator's exact
+        refine runs on the context's refine stream, behind an event."""
+        self.ctx.check(self.ctx.lib.vsig_set_option(self.ctx.h, b"refine_async", int(bool(on))),
+                       "refine_async")
+
+    def refine_stream(self):
+        """The stream the refine runs on, as a torch stream (its consumers --
+        the peak records' all-gather -- are issued there)."""
+        return torch.cuda.ExternalStream(self.ctx.lib.vsig_refine_stream(self.ctx.h), device=self.dev)
+
+    def join_refine(self):
+        """torch's current stream waits for the last refine (an event)."""
+        self.ctx.bind_stream()
+        self.ctx.check(self.ctx.lib.vsig_refine_join(self.ctx.h), "refine_join")
+
 
 class StreamChain:
     """One rank's part of the sharded chain (world = 1: the plain chain)."""
 
     def __init__(self, cfg: ChainConfig, backend, rank: int = 0, world: int = 1, group=None,
-                 transport=None):
+                 transport=None, overlap_refine: bool = False):
+        """overlap_refine: the correlator's exact-argmax refine of step k runs on
+        the backend's refine stream beside step k + 1's FIR (which writes the
+        other of two filtered-stream buffers, the refine re-reading this one);
+        the peak records' all-gather is issued on that stream and global_peak
+        joins it.  Needs a backend with set_overlap_refine (HipBackend); costs
+        a second filtered-stream buffer (4.3 GB at config 5)."""
         cfg.validate(world)
         self.cfg, self.be, self.rank, self.world, self.group = cfg, backend, rank, world, group
         self.tr = transport if transport is not None else TorchTransport(group)
@@ -216,7 +239,13 @@ class StreamChain:
         self.L = len(cfg.template) if cfg.template is not None else 0
         self.yhalo = (self.L - 1) if (self.L and rank < world - 1) else 0
         self.x_ext = backend.empty(self.hist + cfg.n_local)          # [left halo | chunk]
-        self.y_ext = backend.empty(self.ny + max(self.L - 1, 0))     # [chunk out | right halo]
+        self.overlap = bool(overlap_refine and self.L and hasattr(backend, "set_overlap_refine"))
+        if self.overlap:
+            backend.set_overlap_refine(True)
+        # [chunk out | right halo]; two of them with overlap_refine (step k uses
+        # buffer k mod 2, see _begin_step)
+        self._y_bufs = [backend.empty(self.ny + max(self.L - 1, 0))
+                        for _ in range(2 if overlap_refine and self.L else 1)]
         self.sxx = backend.empty((self.ny // cfg.nfft) * cfg.nfft, torch.float32)
         # peak records, double-buffered: the all-gather of step k runs behind
         # step k + 1 (it is waited for only before step k + 2 reuses its slot,
@@ -225,6 +254,7 @@ class StreamChain:
         self._rows = backend.empty(2 * 4 * world, torch.float64).view(2, world * 4)
         self._gather = [None, None]
         self._slot = 1
+        self.y_ext = self._y_bufs[self._slot % len(self._y_bufs)]
         self.peak_rows = None
         self._wt = None                   # exposed-wait events (enable_wait_timing)
 
@@ -278,13 +308,18 @@ class StreamChain:
 
     def _begin_step(self):
         self._slot ^= 1
+        self.y_ext = self._y_bufs[self._slot % len(self._y_bufs)]
         work, self._gather[self._slot] = self._gather[self._slot], None
         if work:
             self._waited("gather", self.tr.wait, work)   # the all-gather two steps back
 
     def _gather_peaks(self):
         rows = self._rows[self._slot]
-        self._gather[self._slot] = self.tr.all_gather_start(rows, self.rec)
+        if self.overlap:          # behind the refine, not in front of the next FIR
+            with torch.cuda.stream(self.be.refine_stream()):
+                self._gather[self._slot] = self.tr.all_gather_start(rows, self.rec)
+        else:
+            self._gather[self._slot] = self.tr.all_gather_start(rows, self.rec)
         return list(rows.view(self.world, 4).unbind(0))
 
     def _exchange_start(self, send, dst, recv, src):
@@ -357,6 +392,8 @@ class StreamChain:
         A refine fault -- on this rank since the last call (the backend's
         sticky fault word) or on any rank (its gathered row's poisoned index,
         refine.hip poison_record) -- raises RefineFault."""
+        if self.overlap:
+            self.be.join_refine()
         self.tr.wait(self._gather[self._slot])
         check = getattr(self.be, "check_refine", None)
         if check is not None:
