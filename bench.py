@@ -419,6 +419,11 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
         lib.vsig_timing_read(h, name.encode(), C.byref(tot), C.byref(cnt))
         if cnt.value:
             stages[name] = tot.value / cnt.value
+    if chain.overlap and "refine" in stages:
+        # beside the next step's FIR the refine's blocks start as FIR waves free
+        # a SIMD's registers, so its span is the FIR's; what the step pays for it
+        # is not this span (ms_per_step against --no-overlap-refine)
+        stages["refine_overlapped_span"] = stages.pop("refine")
     # untimed diagnostic steps after the timed loop (the timed steps stay the
     # single-rank path's): each stage's effective clock, and at world > 1 the
     # exposed waits of the exchanges
@@ -501,13 +506,16 @@ def run_chain_leg(args, n, decim, rank, world, local, dev, steps, warmup):
         stage_roof["xcorr"].update({"flops": int(flops), "TFLOPs": round(tf, 2),
                                     "valu_peak_TFLOPs": FP32_PEAK_TF,
                                     "valu_frac": round(tf / FP32_PEAK_TF, 4), "M": M})
-    if "refine" in stages:
-        # overlapped: the refine's own duration, beside the next step's FIR; the
-        # step's time beyond its three stages is what stays exposed (with the
-        # launch gaps between the stages)
-        stage_roof["refine"] = {"ms": round(stages["refine"], 4), "overlapped": overlapped,
+    if "refine" in stages or "refine_overlapped_span" in stages:
+        # overlapped: the refine runs beside the next step's FIR (its span there
+        # is the FIR's); the step's time beyond its three stages is what stays
+        # exposed of it, with the launch gaps between the stages
+        stage_roof["refine"] = {"overlapped": overlapped,
+                                "ms" if not overlapped else "span_beside_next_fir_ms":
+                                    round(stages.get("refine", stages.get("refine_overlapped_span", 0.0)), 4),
                                 "step_minus_stages_ms": round(
-                                    ms_per_step - sum(stages.get(k, 0.0) for k in ("fir", "psd", "xcorr")), 4)}
+                                    ms_per_step - sum(stages.get(k, 0.0) for k in ("fir", "psd", "xcorr",
+                                                                                    "refine")), 4)}
     # north_star's FIR+FFT target on SURVEY.md §8(d)'s unfused byte count
     # (filter() writes y, spectrum() reads it): 8 + 8/D + 12/D B/sample
     if "fir" in stages and "psd" in stages:

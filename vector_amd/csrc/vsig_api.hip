@@ -654,7 +654,12 @@ int vsig_set_option(vsig_ctx* c, const char* key, int value) {
     c->blas_threads = value;
   } else if (k == "refine_async") {
     if (value && !c->rstream) {
-      HIPCHK(c, hipStreamCreateWithFlags(&c->rstream, hipStreamNonBlocking));
+      // the highest stream priority: the refine's few blocks are dispatched
+      // ahead of the next step's FIR blocks queued beside them (at the default
+      // priority they waited for CU slots behind the FIR and spun for ~3 ms)
+      int lo = 0, hi = 0;
+      if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+      HIPCHK(c, hipStreamCreateWithPriority(&c->rstream, hipStreamNonBlocking, hi));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_corr, hipEventDisableTiming));
       HIPCHK(c, hipEventCreateWithFlags(&c->ev_ref, hipEventDisableTiming));
     }
