@@ -311,6 +311,8 @@ def rank_row(elapsed, steps, stages, waits, clocks=None):
     row = {"ms_per_step": elapsed / steps * 1e3}
     for k in ("fir", "psd", "xcorr", "refine"):
         row[k] = float(stages.get(k, 0.0))
+    if "refine_overlapped_span" in stages:     # the refine beside the next step's FIR
+        row["refine"] = float(stages["refine_overlapped_span"])
     for k in ("left_halo", "right_halo", "gather"):
         row[k + "_wait"] = float(waits.get(k, 0.0))
     for k in CLOCK_STAGES:
