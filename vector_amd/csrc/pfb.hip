@@ -87,6 +87,14 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
       return xg[(int)r * C];
     }
   };
+  // rows only this group reads (walk steps below fpg - PT + 1, either
+  // direction) load non-temporal: they need no L2 residency (round 6 A/B, with
+  // the non-temporal spectrum stores: 1.537-1.540 -> 1.460-1.463 ms, of which
+  // the stores 1.469-1.470, profiles/r06_pfb_ab.txt)
+  auto row_nt = [&](long long r) -> float2 {
+    const f2v q = __builtin_nontemporal_load(reinterpret_cast<const f2v*>(xg + (int)r * C));
+    return fromv(q);
+  };
   constexpr bool PF = (VAR & 2) != 0;
   // FFT role of this thread: frame slot ff of the batch, thread t of the frame,
   // frames across the lanes (ff = tid mod FB): the 16 lanes of an LDS access
@@ -161,6 +169,10 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
           if (!(last && u == U - 1)) {                        // next batch
             if (X && u == 0 && last) {                        // only its row 0 from HBM
               nxt[0] = row(newrow(b + (u + 1) * E), chkc);
+            } else if (!decltype(chkc)::value &&
+                       b + (u + 2) * E <= fpg - PT + 1) {   // rows no other group reads
+#pragma unroll
+              for (int i = 0; i < E; ++i) nxt[i] = row_nt(newrow(b + (u + 1) * E + i));
             } else {
 #pragma unroll
               for (int i = 0; i < E; ++i) nxt[i] = row(newrow(b + (u + 1) * E + i), chkc);
@@ -180,7 +192,10 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
 #pragma unroll
         for (int i = 0; i < E; ++i) {
           const long long m = mf(b + u * E + i);
-          if (m < M) y[m * C + p] = lds[(g * E + i) * S + lpad(p)];
+          // spectra leave non-temporal: written once, never re-read here
+          if (m < M)
+            __builtin_nontemporal_store(tov(lds[(g * E + i) * S + lpad(p)]),
+                                        reinterpret_cast<f2v*>(y + m * C + p));
         }
         __syncthreads();                                      // lds reused by the next batch
       });
@@ -206,7 +221,10 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
 // again in round 6 with the row exchange: 128 +9 %, 32 +0.1..1 %; VAR 3 +1 %,
 // profiles/r06_pfb_ab.txt).
 constexpr int kPfbVar64 = 7;
-constexpr long long kPfbFramesPerGroup = 64;
+#ifndef VSIG_PFB_FPG
+#define VSIG_PFB_FPG 64
+#endif
+constexpr long long kPfbFramesPerGroup = VSIG_PFB_FPG;
 template <class PL, int PT>
 static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
                          const float2* tw, hipStream_t st) {
