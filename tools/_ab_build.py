@@ -10,8 +10,6 @@ from vector_amd import _build  # noqa: E402
 # recorded in DESIGN.md, see round 3's list)
 VARIANTS = {
     "libvsig_rtrace": ("VSIG_REFINE_TRACE=1",),
-    "libvsig_fpg32": ("VSIG_PFB_FPG=32",),
-    "libvsig_fpg128": ("VSIG_PFB_FPG=128",),
 }
 # name -> {source: extra compiler flags} (code-generation A/Bs)
 FLAG_VARIANTS = {

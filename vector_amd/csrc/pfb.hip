@@ -218,13 +218,10 @@ __global__ __launch_bounds__(256, (VAR & 4) ? 4 : 1) void pfb_kernel(const float
 // Shipped configuration: LDS-staged stores + next-batch prefetch (VAR 3;
 // C = 64: registers capped for 4 waves / SIMD, VAR 7: 128 VGPRs, no scratch),
 // 64 frames per group (128 / 256 / 512 measured slower, profiles/r02_v13_pfb_ab.txt;
-// again in round 6 with the row exchange: 128 +9 %, 32 +0.1..1 %; VAR 3 +1 %,
-// profiles/r06_pfb_ab.txt).
+// again in round 6 with the row exchange: 128 +9 %, 32 +0.1..1 %; VAR 3 +1 %;
+// with the non-temporal policy 128 +11 %, 32 +3 %, profiles/r06_pfb_ab.txt).
 constexpr int kPfbVar64 = 7;
-#ifndef VSIG_PFB_FPG
-#define VSIG_PFB_FPG 64
-#endif
-constexpr long long kPfbFramesPerGroup = VSIG_PFB_FPG;
+constexpr long long kPfbFramesPerGroup = 64;
 template <class PL, int PT>
 static void launch_pfb_t(const float2* x, long long n, const float* h, long long M, float2* y,
                          const float2* tw, hipStream_t st) {

@@ -368,7 +368,9 @@ class StreamChain:
         while the halo is in flight, then the correlator once it has landed,
         then the peak records' all-gather (asynchronous, see __init__).
         (Three-stream and sub-chunked pipelines measured slower on MI355X:
-        DESIGN.md section 5.)"""
+        DESIGN.md section 5; so did the PSD after the correlator, +0.7-1.3 %:
+        the stage right after the FIR runs at the lowest clock, and the
+        correlator pays more for it than the PSD, profiles/r06_stage_order_ab.txt.)"""
         self._begin_step()
         r, w, ny, L = self.rank, self.world, self.ny, self.L
         be = self.be
